@@ -1,0 +1,249 @@
+/*
+ * yart.h — C ABI of the MI355X (gfx950) path-tracing core.
+ *
+ * This is the drop-in boundary for the reference's per-pixel-sample render loop
+ * (themayflyman/yet-another-raytracer, raytracer/src/main.rs:649-730, the closure each
+ * thread-pool job runs). The reference has no FFI of its own: its path sits behind the Rust
+ * traits `Hittable` (hittable.rs:11-35), `Material` (material.rs:20-31), `Texture`
+ * (texture.rs:13-16), `Pdf` (pdf.rs:10-13) and `Camera::get_ray` (camera.rs:82-94). A host
+ * that keeps those types (the reference's own Rust, or this repo's C++ mirror under
+ * yet-another-raytracer_amd/host/) walks its scene tree once, flattens it into the plain
+ * structs below and makes ONE call per frame (or per device shard). See INTEGRATION.md for
+ * the Rust `extern "C"` binding a maintainer would add.
+ *
+ * Conventions
+ *  - Every entry point returns 0 (YART_OK) or a negative yart_status; the message of the
+ *    last failure on the calling thread is yart_last_error(). Nothing unwinds across the ABI
+ *    (the reference panics instead: triangle.rs:113, main.rs:557, main.rs:774).
+ *  - All inputs are caller-owned and copied during the call; outputs are caller-allocated.
+ *  - Scene handles are immutable after yart_scene_create and may be used from several host
+ *    threads at once (each call uses the stream it is given).
+ *  - Arithmetic is IEEE f64 throughout, as in the reference (no FMA contraction).
+ */
+#ifndef YART_H
+#define YART_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YART_ABI_VERSION 1u
+
+typedef enum yart_status {
+  YART_OK = 0,
+  YART_ERR_INVALID = -1,     /* bad argument / malformed scene description          */
+  YART_ERR_DEVICE = -2,      /* HIP runtime or kernel failure                        */
+  YART_ERR_NO_MEMORY = -3,   /* host or device allocation failed                     */
+  YART_ERR_UNSUPPORTED = -4, /* a feature outside this build's scope                 */
+  YART_ERR_IO = -5           /* file could not be read / written (host helpers only) */
+} yart_status;
+
+/* ---------------------------------------------------------------- textures (texture.rs) */
+enum {
+  YART_TEX_SOLID = 0,  /* SolidColor<RGB>            texture.rs:18-40 */
+  YART_TEX_CHECKER = 1 /* CheckerTexture<RGB>        texture.rs:42-68 */
+};
+typedef struct yart_texture {
+  uint32_t kind;
+  uint32_t reserved;
+  double rgb[3];      /* SOLID: the colour.  CHECKER: the `odd` colour (sines < 0). */
+  double rgb_even[3]; /* CHECKER: the `even` colour.                                */
+} yart_texture;
+
+/* --------------------------------------------------------------- materials (material.rs) */
+enum {
+  YART_MAT_NONE = 0,          /* NoMaterial          material.rs:383-386 */
+  YART_MAT_LAMBERTIAN = 1,    /* Lambertian<T>       material.rs:33-61   */
+  YART_MAT_METAL = 2,         /* Metal<T>            material.rs:63-95   */
+  YART_MAT_DIELECTRIC = 3,    /* Dielectric          material.rs:111-301 (Sellmeier b, c in nm^2) */
+  YART_MAT_DIFFUSE_LIGHT = 4  /* DiffuseLight<T>     material.rs:336-355 */
+};
+typedef struct yart_material {
+  uint32_t kind;
+  uint32_t texture; /* index into yart_scene_desc.textures (LAMBERTIAN, METAL, DIFFUSE_LIGHT) */
+  double fuzz;      /* METAL */
+  double b[3];      /* DIELECTRIC Sellmeier B1..B3 */
+  double c[3];      /* DIELECTRIC Sellmeier C1..C3 (nm^2, e.g. SF66 c1 = 0.0147053225e6) */
+} yart_material;
+
+/* ------------------------------------------------------------------------- objects */
+enum {
+  YART_PRIM_SPHERE = 0,   /* StillSphere      sphere.rs:31-119   p = cx, cy, cz, radius      */
+  YART_PRIM_XY_RECT = 1,  /* XYRect           aarect.rs:9-77     p = x0, x1, y0, y1, k       */
+  YART_PRIM_XZ_RECT = 2,  /* XZRect           aarect.rs:79-172   p = x0, x1, z0, z1, k       */
+  YART_PRIM_YZ_RECT = 3,  /* YZRect           aarect.rs:174-242  p = y0, y1, z0, z1, k       */
+  YART_PRIM_BOX = 4,      /* BoxEntity        box_entity.rs      p = p0 xyz, p1 xyz          */
+  YART_PRIM_TRIANGLE = 5, /* Triangle         triangle.rs:19-102 p = v0 v1 v2 (9), n0 n1 n2 (9), uv0 uv1 uv2 (6) */
+  YART_PRIM_MESH = 6      /* TriangleMesh     triangle.rs:104-185 (L4QBVH, qbvh.rs:244-544); `mesh` selects the triangles */
+};
+enum {
+  YART_XF_TRANSLATE = 1, /* Translate  hittable.rs:125-163  v = offset            */
+  YART_XF_ROTATE_Y = 2,  /* RotateY    hittable.rs:165-256  v[0] = angle, degrees */
+  YART_XF_FLIP_FACE = 3  /* FlipFace   hittable.rs:328-354                        */
+};
+typedef struct yart_xform {
+  uint32_t kind;
+  uint32_t reserved;
+  double v[3];
+} yart_xform;
+
+#define YART_MAX_XFORMS 4
+typedef struct yart_object {
+  uint32_t kind;     /* YART_PRIM_* */
+  uint32_t material; /* index into materials; a MESH object's triangles all share it, as
+                        TriangleMesh::from_obj gives every triangle one material (triangle.rs:111) */
+  uint32_t mesh;     /* MESH: index into yart_scene_desc.meshes; two objects may share a mesh */
+  uint32_t n_xforms; /* wrappers around the primitive, OUTERMOST first:
+                        Translate(RotateY(Box)) = { TRANSLATE, ROTATE_Y } */
+  yart_xform xforms[YART_MAX_XFORMS];
+  double p[24];
+} yart_object;
+
+/* A triangle soup as TriangleMesh::from_obj produces it (triangle.rs:111-174): positions are
+ * the f32 values tobj parsed, normals/uvs already defaulted (face normal / (0,0)). */
+typedef struct yart_mesh {
+  uint32_t n_triangles;
+  uint32_t reserved;
+  const float* positions; /* n_triangles * 9 : v0 xyz, v1 xyz, v2 xyz                 */
+  const double* normals;  /* n_triangles * 9 : n0, n1, n2 (not normalised, as stored) */
+  const double* uvs;      /* n_triangles * 6 or NULL (u/v are not read by in-scope textures) */
+} yart_mesh;
+
+typedef struct yart_scene_desc {
+  uint32_t abi_version; /* = YART_ABI_VERSION */
+  uint32_t n_objects;
+  uint32_t n_lights;
+  uint32_t n_materials;
+  uint32_t n_textures;
+  uint32_t n_meshes;
+  const yart_object* objects;   /* the world HittableList, in insertion order (scenes.rs)   */
+  const yart_object* lights;    /* the `lights` HittableList (main.rs:221), in order; only
+                                   bare XZ_RECT and SPHERE entries carry a pdf (aarect.rs:148-171,
+                                   sphere.rs:95-118), every other entry pdf 0 (hittable.rs:28-34) */
+  const yart_material* materials;
+  const yart_texture* textures;
+  const yart_mesh* meshes;
+  double background[3]; /* background RGB, reflected spectrally on a miss (main.rs:587) */
+} yart_scene_desc;
+
+/* Camera (camera.rs:10-23). Fill with yart_camera_init (camera.rs:41-80). */
+typedef struct yart_camera {
+  double lower_left_corner[3];
+  double horizontal[3];
+  double vertical[3];
+  double origin[3];
+  double u[3];
+  double v[3];
+  double w[3];
+  double lens_radius;
+  double time0;
+  double time1;
+} yart_camera;
+
+/* One frame (or one shard of it). The reference renders the pixels covered by its fixed 8x8
+ * grid of crop rectangles (main.rs:628-647): pixels outside every crop (e.g. row 224 of a
+ * 225-row image) are never sampled, their sums stay 0 and finalize leaves them RGBA 0,0,0,0.
+ * Work is dealt to devices in 8x8-pixel blocks: block b (row-major over ceil(W/8) x ceil(H/8))
+ * is rendered by the shard with b % shard_count == shard_index. */
+typedef struct yart_render_params {
+  uint32_t width;
+  uint32_t height;
+  uint32_t spp;       /* samples_per_pixel */
+  uint32_t max_depth; /* ray_color depth    */
+  uint64_t seed;      /* counter-based RNG key (Philox4x32-10); the reference's thread_rng()
+                         is unseedable, see DESIGN.md "RNG" */
+  uint32_t shard_index;
+  uint32_t shard_count; /* 0 or 1 = whole frame */
+} yart_render_params;
+
+typedef struct yart_scene yart_scene; /* opaque, device resident */
+
+typedef struct yart_scene_info {
+  int device;
+  uint32_t n_objects;
+  uint32_t n_lights;
+  uint32_t n_meshes;
+  uint32_t bvh_nodes;     /* inner QBVH nodes over all meshes (qbvh.rs:547-554)        */
+  uint32_t bvh_leaves;    /* leaves (<= 4 triangles each, qbvh.rs:261-279)              */
+  uint32_t bvh_max_depth; /* deepest root-to-leaf path in inner nodes                   */
+  uint32_t bvh_max_stack; /* traversal stack slots the deepest path can need            */
+  uint64_t device_bytes;  /* HBM held by the scene                                      */
+} yart_scene_info;
+
+/* Per-launch work counters (optional, for roofline accounting; they slow the kernel). */
+typedef struct yart_render_stats {
+  uint64_t samples;        /* camera samples completed                           */
+  uint64_t segments;       /* world.hit calls on path rays (hittable.rs:67)      */
+  uint64_t prim_tests;     /* analytic primitive tests (sphere/rect/triangle)    */
+  uint64_t node_visits;    /* QBVH inner nodes tested (4 boxes each)             */
+  uint64_t leaf_visits;    /* QBVH leaves tested (<= 4 triangles each)           */
+  uint64_t leaf_tris;      /* triangles tested inside leaves                     */
+  uint64_t light_tests;    /* primitive hits re-run by pdf_value (pdf.rs:452)    */
+  uint64_t reserved[9];
+} yart_render_stats;
+
+typedef void (*yart_progress_fn)(uint64_t pixels_done, void* user);
+
+/* ------------------------------------------------------------------------ entry points */
+const char* yart_version(void);
+const char* yart_last_error(void); /* thread-local; "" when the last call succeeded */
+
+int yart_device_count(int* out);
+
+/* Copies the description to `device` (HBM), building the mesh QBVHs (qbvh.rs:252-361). */
+int yart_scene_create(int device, const yart_scene_desc* desc, yart_scene** out);
+void yart_scene_destroy(yart_scene* scene);
+int yart_scene_get_info(const yart_scene* scene, yart_scene_info* out);
+
+/* camera.rs:41-80 (host arithmetic, f64). */
+int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lookat[3],
+                     const double vup[3], double vfov_degrees, double aspect_ratio,
+                     double aperture, double focus_dist, double time0, double time1);
+
+/* Render into a DEVICE buffer on a caller stream (hipStream_t, NULL = default stream).
+ * d_xyz_sum: width*height*3 doubles on the scene's device, per-pixel sums of the sanitised
+ * sample XYZ (main.rs:690-708). Only this shard's blocks are written; the caller zeroes the
+ * buffer if it wants the rest to read 0. Asynchronous: returns after the launch. */
+int yart_render_async(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
+                      double* d_xyz_sum, void* hip_stream);
+
+/* Same, with host output and an optional progress callback (called on this thread). */
+int yart_render(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
+                double* xyz_sum_out, yart_progress_fn progress, void* user);
+
+/* Instrumented render (same image) that also returns the work counters. Host output. */
+int yart_render_with_stats(yart_scene* scene, const yart_camera* cam,
+                           const yart_render_params* p, double* xyz_sum_out,
+                           yart_render_stats* stats);
+
+/* main.rs:710-718: xyz * 360 / (CIE_Y_INTERGAL * spp) -> XYZ::into_rgb -> sRGB gamma ->
+ * (256 * clamp(c, 0, 0.999)) as u8, alpha 255; pixels the tile grid never covers -> 0,0,0,0.
+ * Device buffers, caller stream. */
+int yart_finalize_rgba8_async(int device, const double* d_xyz_sum, uint32_t width,
+                              uint32_t height, uint32_t spp, uint8_t* d_rgba, void* hip_stream);
+int yart_finalize_rgba8(int device, const double* xyz_sum, uint32_t width, uint32_t height,
+                        uint32_t spp, uint8_t* rgba_out); /* host buffers */
+
+/* Batched closest hit against the world list: the `Hittable::hit` boundary
+ * (hittable.rs:24, HittableList::hit hittable.rs:67-79), on the device.
+ * rays: n * 8 doubles (origin xyz, direction xyz, t_min, t_max).
+ * hits: n * 8 doubles (t, p xyz, normal xyz, front_face 0/1); obj: n ints, the index of the
+ * world object hit or -1 (then hits[] is left as NaN). Host buffers. */
+int yart_intersect(yart_scene* scene, const double* rays, uint32_t n, double* hits,
+                   int32_t* obj);
+
+/* Test probes (device side of the parity tests). */
+/* The per-sample random stream: n draws of gen::<f64>() for (pixel, sample). */
+int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n,
+                   double* out);
+/* Elementwise device math on n inputs: op 0 sqrt(a), 1 a/b, 2 sin(a), 3 cos(a), 4 pow(a,b). */
+int yart_probe_math(int device, int op, const double* a, const double* b, uint32_t n,
+                    double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YART_H */

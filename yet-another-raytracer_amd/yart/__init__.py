@@ -1,0 +1,217 @@
+"""Python glue over the two C ABIs (include/yart.h, include/yart_host.h).
+
+The product is the HIP library libyart.so (kernels + C ABI) and the C++ host layer
+libyart_host.so (presets, OBJ loading, CLI resolution); this module only loads them with
+ctypes for tests, bench.py and smoke(). If torch is going to be used in the same process,
+import it BEFORE load_device() so libyart.so binds to the HIP runtime torch already loaded
+(both carry the soname libamdhip64.so.7) and device pointers are shared.
+"""
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+from . import abi
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+REPO_DIR = PKG_DIR.parent
+LIB_DIR = PKG_DIR / "lib"
+ASSET_DIR = REPO_DIR / "assets"
+DEFAULT_SEED = 0x59415254  # counter RNG seed for every run
+
+_host = None
+_dev = None
+
+
+class YartError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"yart error {code}: {msg}")
+        self.code = code
+
+
+def _sig(lib, name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+
+
+def load_host():
+    """libyart_host.so (C++, no GPU)."""
+    global _host
+    if _host is not None:
+        return _host
+    path = LIB_DIR / "libyart_host.so"
+    if not path.exists():
+        raise FileNotFoundError(f"{path} is not built; run `make` (or __graft_entry__.build())")
+    L = C.CDLL(str(path))
+    P, U32, U64, D, I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_double, C.c_int
+    _sig(L, "yart_preset_create", I, C.c_char_p, C.c_char_p, U64, C.POINTER(P))
+    _sig(L, "yart_preset_destroy", None, P)
+    _sig(L, "yart_preset_desc", C.POINTER(abi.SceneDesc), P)
+    _sig(L, "yart_preset_defaults", I, P, C.POINTER(abi.RenderDefaults))
+    _sig(L, "yart_preset_stand_in", C.c_char_p, P)
+    _sig(L, "yart_scene_names", I, C.POINTER(C.c_char_p), I)
+    _sig(L, "yart_resolve_dimensions", None, U32, U32, U32, U32, C.POINTER(U32), C.POINTER(U32))
+    _sig(L, "yart_cli_parse", I, I, C.POINTER(C.c_char_p), C.POINTER(abi.Cli))
+    _sig(L, "yart_resolve_render_options", I, C.c_char_p, C.POINTER(abi.RenderDefaults), C.POINTER(abi.Cli),
+         C.POINTER(abi.RenderOptions))
+    _sig(L, "yart_obj_triangle_count", I, C.c_char_p, C.POINTER(U32))
+    _sig(L, "yart_obj_load", I, C.c_char_p, P, P, P, U32)
+    _sig(L, "yart_write_png", I, C.c_char_p, P, U32, U32)
+    _sig(L, "yart_host_camera_init", I, C.POINTER(abi.Camera), P, P, P, D, D, D, D, D, D)
+    _sig(L, "yart_host_last_error", C.c_char_p)
+    _host = L
+    return L
+
+
+def load_device():
+    """libyart.so (HIP kernels for gfx950 + C ABI). Raises if it is not built."""
+    global _dev
+    if _dev is not None:
+        return _dev
+    path = LIB_DIR / "libyart.so"
+    if not path.exists():
+        raise FileNotFoundError(f"{path} is not built; the HIP path has no fallback")
+    L = C.CDLL(str(path))
+    P, U32, U64, D, I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_double, C.c_int
+    _sig(L, "yart_version", C.c_char_p)
+    _sig(L, "yart_last_error", C.c_char_p)
+    _sig(L, "yart_device_count", I, C.POINTER(I))
+    _sig(L, "yart_scene_create", I, I, C.POINTER(abi.SceneDesc), C.POINTER(P))
+    _sig(L, "yart_scene_destroy", None, P)
+    _sig(L, "yart_scene_get_info", I, P, C.POINTER(abi.SceneInfo))
+    _sig(L, "yart_camera_init", I, C.POINTER(abi.Camera), P, P, P, D, D, D, D, D, D)
+    _sig(L, "yart_render_async", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, P)
+    _sig(L, "yart_render", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, abi.PROGRESS_FN, P)
+    _sig(L, "yart_render_with_stats", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P,
+         C.POINTER(abi.RenderStats))
+    _sig(L, "yart_finalize_rgba8_async", I, I, P, U32, U32, U32, P, P)
+    _sig(L, "yart_finalize_rgba8", I, I, P, U32, U32, U32, P)
+    _sig(L, "yart_intersect", I, P, P, U32, P, P)
+    _sig(L, "yart_probe_rng", I, I, U64, U32, U32, U32, P)
+    _sig(L, "yart_probe_math", I, I, I, P, P, U32, P)
+    _dev = L
+    return L
+
+
+def _check_host(rc):
+    if rc != 0:
+        raise YartError(rc, load_host().yart_host_last_error().decode())
+
+
+def _check_dev(rc):
+    if rc != 0:
+        raise YartError(rc, load_device().yart_last_error().decode())
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Preset:
+    """build_scene_preset (main.rs:211-432) through libyart_host; owns the flattened desc."""
+
+    def __init__(self, name, asset_dir=None, scene_seed=42):
+        H = load_host()
+        self._h = C.c_void_p()
+        _check_host(H.yart_preset_create(name.encode(), str(asset_dir or ASSET_DIR).encode(), scene_seed,
+                                         C.byref(self._h)))
+        self.name = name
+        self.desc = H.yart_preset_desc(self._h)
+        d = abi.RenderDefaults()
+        _check_host(H.yart_preset_defaults(self._h, C.byref(d)))
+        self.defaults = d
+        self.stand_in = H.yart_preset_stand_in(self._h).decode()
+
+    def close(self):
+        if self._h:
+            load_host().yart_preset_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def camera(self, width, height, vfov=None, aperture=None):
+        """render()'s camera (main.rs:610-626): vup (0,1,0), focus 10, shutter [0, 1)."""
+        return make_camera(self.defaults.lookfrom, self.defaults.lookat, vfov if vfov is not None else self.defaults.vfov,
+                           width / height, aperture if aperture is not None else self.defaults.aperture)
+
+
+def make_camera(lookfrom, lookat, vfov, aspect, aperture, focus_dist=10.0, vup=(0.0, 1.0, 0.0)):
+    cam = abi.Camera()
+    lf = (C.c_double * 3)(*lookfrom)
+    la = (C.c_double * 3)(*lookat)
+    up = (C.c_double * 3)(*vup)
+    _check_host(load_host().yart_host_camera_init(C.byref(cam), lf, la, up, vfov, aspect, aperture, focus_dist, 0.0, 1.0))
+    return cam
+
+
+def render_params(width, height, spp, max_depth, seed=DEFAULT_SEED, shard_index=0, shard_count=1):
+    return abi.RenderParams(width, height, spp, max_depth, seed, shard_index, shard_count)
+
+
+class DeviceScene:
+    """A scene resident in one GPU's HBM (yart_scene_create)."""
+
+    def __init__(self, desc, device=0):
+        L = load_device()
+        self._s = C.c_void_p()
+        _check_dev(L.yart_scene_create(device, desc, C.byref(self._s)))
+        self.device = device
+
+    def close(self):
+        if self._s:
+            load_device().yart_scene_destroy(self._s)
+            self._s = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        i = abi.SceneInfo()
+        _check_dev(load_device().yart_scene_get_info(self._s, C.byref(i)))
+        return i
+
+    def render(self, cam, params):
+        out = np.zeros((params.height, params.width, 3), dtype=np.float64)
+        _check_dev(load_device().yart_render(self._s, C.byref(cam), C.byref(params), _ptr(out), abi.PROGRESS_FN(0), None))
+        return out
+
+    def render_with_stats(self, cam, params):
+        out = np.zeros((params.height, params.width, 3), dtype=np.float64)
+        st = abi.RenderStats()
+        _check_dev(load_device().yart_render_with_stats(self._s, C.byref(cam), C.byref(params), _ptr(out), C.byref(st)))
+        return out, st
+
+    def render_async(self, cam, params, d_xyz_ptr, stream_ptr):
+        _check_dev(load_device().yart_render_async(self._s, C.byref(cam), C.byref(params), C.c_void_p(d_xyz_ptr),
+                                                  C.c_void_p(stream_ptr)))
+
+    def intersect(self, rays):
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
+        n = rays.shape[0]
+        hits = np.empty((n, 8), dtype=np.float64)
+        obj = np.empty(n, dtype=np.int32)
+        _check_dev(load_device().yart_intersect(self._s, _ptr(rays), n, _ptr(hits), _ptr(obj)))
+        return hits, obj
+
+
+def finalize_rgba8(xyz_sum, spp, device=0):
+    h, w, _ = xyz_sum.shape
+    xyz = np.ascontiguousarray(xyz_sum, dtype=np.float64)
+    out = np.zeros((h, w, 4), dtype=np.uint8)
+    _check_dev(load_device().yart_finalize_rgba8(device, _ptr(xyz), w, h, spp, _ptr(out)))
+    return out
+
+
+def write_png(path, rgba):
+    rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+    h, w, _ = rgba.shape
+    _check_host(load_host().yart_write_png(str(path).encode(), _ptr(rgba), w, h))

@@ -1,0 +1,100 @@
+"""ctypes mirror of include/yart.h and include/yart_host.h (layout must match the C headers)."""
+import ctypes as C
+
+ABI_VERSION = 1
+
+OK, ERR_INVALID, ERR_DEVICE, ERR_NO_MEMORY, ERR_UNSUPPORTED, ERR_IO = 0, -1, -2, -3, -4, -5
+
+TEX_SOLID, TEX_CHECKER = 0, 1
+MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT = 0, 1, 2, 3, 4
+PRIM_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT, PRIM_BOX, PRIM_TRIANGLE, PRIM_MESH = range(7)
+XF_TRANSLATE, XF_ROTATE_Y, XF_FLIP_FACE = 1, 2, 3
+MAX_XFORMS = 4
+
+D3 = C.c_double * 3
+
+
+class Texture(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("rgb", D3), ("rgb_even", D3)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("texture", C.c_uint32), ("fuzz", C.c_double), ("b", D3), ("c", D3)]
+
+
+class Xform(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("v", D3)]
+
+
+class Object(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("material", C.c_uint32), ("mesh", C.c_uint32), ("n_xforms", C.c_uint32),
+                ("xforms", Xform * MAX_XFORMS), ("p", C.c_double * 24)]
+
+
+class Mesh(C.Structure):
+    _fields_ = [("n_triangles", C.c_uint32), ("reserved", C.c_uint32), ("positions", C.POINTER(C.c_float)),
+                ("normals", C.POINTER(C.c_double)), ("uvs", C.POINTER(C.c_double))]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("n_objects", C.c_uint32), ("n_lights", C.c_uint32),
+                ("n_materials", C.c_uint32), ("n_textures", C.c_uint32), ("n_meshes", C.c_uint32),
+                ("objects", C.POINTER(Object)), ("lights", C.POINTER(Object)),
+                ("materials", C.POINTER(Material)), ("textures", C.POINTER(Texture)),
+                ("meshes", C.POINTER(Mesh)), ("background", D3)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("lower_left_corner", D3), ("horizontal", D3), ("vertical", D3), ("origin", D3),
+                ("u", D3), ("v", D3), ("w", D3), ("lens_radius", C.c_double), ("time0", C.c_double),
+                ("time1", C.c_double)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32),
+                ("seed", C.c_uint64), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("device", C.c_int), ("n_objects", C.c_uint32), ("n_lights", C.c_uint32), ("n_meshes", C.c_uint32),
+                ("bvh_nodes", C.c_uint32), ("bvh_leaves", C.c_uint32), ("bvh_max_depth", C.c_uint32),
+                ("bvh_max_stack", C.c_uint32), ("device_bytes", C.c_uint64)]
+
+
+class RenderStats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("leaf_tris", C.c_uint64),
+                ("light_tests", C.c_uint64), ("reserved", C.c_uint64 * 9)]
+
+
+class RenderDefaults(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("samples_per_pixel", C.c_uint64),
+                ("max_depth", C.c_uint64), ("workers", C.c_uint64), ("vfov", C.c_double), ("aperture", C.c_double),
+                ("lookfrom", D3), ("lookat", D3), ("background", D3), ("output_filename", C.c_char * 64)]
+
+
+class Cli(C.Structure):
+    _fields_ = [("scene", C.c_char * 64), ("output", C.c_char * 512), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("samples", C.c_uint64), ("max_depth", C.c_uint64), ("workers", C.c_uint64), ("vfov", C.c_double),
+                ("aperture", C.c_double), ("seed", C.c_uint64), ("gpus", C.c_int32), ("assets", C.c_char * 512)]
+
+
+class RenderOptions(C.Structure):
+    _fields_ = [("output_path", C.c_char * 512), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("samples_per_pixel", C.c_uint64), ("max_depth", C.c_uint64), ("workers", C.c_uint64),
+                ("vfov", C.c_double), ("aperture", C.c_double)]
+
+
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_uint64, C.c_void_p)
+
+# Every symbol include/yart.h declares (checked by tests/test_abi.py without a GPU).
+DEVICE_SYMBOLS = [
+    "yart_version", "yart_last_error", "yart_device_count", "yart_scene_create", "yart_scene_destroy",
+    "yart_scene_get_info", "yart_camera_init", "yart_render_async", "yart_render", "yart_render_with_stats",
+    "yart_finalize_rgba8_async", "yart_finalize_rgba8", "yart_intersect", "yart_probe_rng", "yart_probe_math",
+]
+HOST_SYMBOLS = [
+    "yart_preset_create", "yart_preset_destroy", "yart_preset_desc", "yart_preset_defaults", "yart_preset_stand_in",
+    "yart_scene_names", "yart_resolve_dimensions", "yart_cli_parse", "yart_resolve_render_options",
+    "yart_obj_triangle_count", "yart_obj_load", "yart_write_png", "yart_host_camera_init", "yart_host_last_error",
+]
