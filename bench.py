@@ -1,0 +1,186 @@
+"""bench.py — BASELINE.json's headline metric on MI355X.
+
+Metric: Msamples/s (W x H x spp / s) for cornell-box 800x800, 256 spp, depth 50 (configs[1]);
+ms_per_step is the wall-clock of one frame. A step = one frame of the hot path: every rank
+renders its share of 8x8-pixel blocks (block b -> rank b % N) with the HIP megakernel through the
+C ABI (yart_render_async), the shards are summed into rank 0's frame with ONE RCCL reduce over
+xGMI (N > 1), and rank 0 runs finalize (XYZ -> sRGB RGBA8). Inputs (scene, BVH, camera) are
+resident in HBM before the timed region. Scaling is strong: the frame is fixed as N grows.
+
+Also reported on the same line:
+  roofline      the render kernel's average launch duration (HIP events on the stream it runs on)
+                against the f64 VALU peak, with algorithmic FLOPs from the kernel's own work
+                counters (an untimed instrumented launch of the same frame) x the per-operation
+                FLOP model in DESIGN.md; HBM traffic from the committed rocprofv3 PMC summary.
+  cpu_baseline  the CPU restatement (oracle/) on this host's cores, rank 0 only, on a bounded
+                sample of the same workload (same frame at fewer spp; Msamples/s is ~spp-invariant).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch  # first: libyart.so binds to the HIP runtime torch loaded (shared device pointers)
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
+import yart  # noqa: E402
+
+WORKLOAD = dict(scene="cornell-box", width=800, height=800, spp=256, max_depth=50)
+
+# f64 FLOPs per counted operation (DESIGN.md "Roofline"): add/sub/mul/div/sqrt = 1, compares 0.
+FLOPS = {
+    "sample": 40,        # jitter, wavelength, camera ray, CIE lookup, sanitize, accumulate
+    "segment": 150,      # hit-record wrappers + material scatter + mixture pdf + ONB
+    "prim": 14,          # average analytic primitive test (rect 8, sphere 28)
+    "node": 96,          # QBVH inner node: 4 children x 3 axes slab (sub, mul) x 2 + min/max
+    "leaf_tri": 45,      # Moller-Trumbore in f64
+    "light": 30,         # pdf_value re-test of a light (rect 20, sphere 38)
+}
+F64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec, FMA = 2 FLOPs)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
+    ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
+    return ap.parse_args()
+
+
+def cpu_baseline(preset, cam, w, h, spp, depth, threads):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    scene = O.OracleScene(preset.desc)
+    prm = yart.render_params(w, h, spp, depth)
+    t0 = time.perf_counter()
+    scene.render(cam, prm, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h * spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{WORKLOAD['scene']} {w}x{h}x{spp}spp depth {depth} (full frame, reduced spp), "
+                      f"{dt:.2f} s on {threads} threads, oracle/ C restatement"}
+
+
+def pmc_traffic():
+    """HBM bytes per render launch from the committed rocprofv3 PMC summary, if present."""
+    p = ROOT / "profiles" / "pmc_render_cornell.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    W, H, spp, depth = WORKLOAD["width"], WORKLOAD["height"], WORKLOAD["spp"], WORKLOAD["max_depth"]
+
+    preset = yart.Preset(WORKLOAD["scene"])
+    cam = preset.camera(W, H)
+    prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world)
+    scene = yart.DeviceScene(preset.desc, device=local)
+    mine = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)   # this rank's blocks, zeros elsewhere
+    frame = torch.zeros_like(mine) if world > 1 else mine
+    rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    L = yart.load_device()
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        scene.render_async(cam, prm, mine.data_ptr(), stream.cuda_stream)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            frame.copy_(mine)
+            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
+                                             yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(stream.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(L.yart_last_error().decode())
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / max(1, len(ev))
+
+    # the image really is the frame (cheap sanity: finite, non-zero)
+    if rank == 0:
+        f = frame.float()
+        assert torch.isfinite(f).all() and f.abs().sum() > 0
+
+    roofline = None
+    cpu = None
+    if rank == 0 and not a.no_stats:
+        _, st = scene.render_with_stats(cam, yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world))
+        flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
+                 st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        traffic = pmc_traffic()
+        roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / F64_VALU_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "kernel": "k_render<false,false>", "kernel_ms": round(kern_ms, 3),
+                    "algorithmic_flops_per_launch": int(flops),
+                    "counts": {"samples": st.samples, "segments": st.segments, "prim_tests": st.prim_tests,
+                               "light_tests": st.light_tests, "node_visits": st.node_visits,
+                               "leaf_tris": st.leaf_tris},
+                    "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None)}
+    if rank == 0 and a.cpu_spp > 0 and world == 1:
+        cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
+
+    if rank == 0:
+        samples = W * H * spp
+        value = samples * a.steps / elapsed / 1e6
+        line = {
+            "metric": "Msamples/sec (WxHxspp/sec), cornell-box 800x800x256spp depth 50",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
+            "config": {"workload": "cornell-box 800x800x256spp depth 50 (BASELINE configs[1])", "width": W,
+                       "height": H, "spp": spp, "max_depth": depth, "parallelism": f"pixel-blocks x{world}",
+                       "seed": yart.DEFAULT_SEED},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

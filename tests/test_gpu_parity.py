@@ -1,0 +1,176 @@
+"""Parity of the HIP path (libyart.so on the MI355X) against the CPU restatement (oracle).
+
+Both sides evaluate the reference's hot path in IEEE f64 with the same counter-based RNG, so the
+bar is BITWISE equality, not a tolerance: every pixel sum, every hit record, every random draw.
+The only arithmetic the two do not share is libm's pow in finalize (ocml vs glibc), where the
+8-bit output is allowed to differ by 1 LSB on at most 0.1 % of channels.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import yart
+from yart import abi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    L = yart.load_device()
+    n = C.c_int()
+    assert L.yart_device_count(C.byref(n)) == 0 and n.value >= 1, L.yart_last_error()
+    return L
+
+
+def test_rng_stream_bitwise(dev):
+    for seed, pixel, sample in [(0x59415254, 0, 0), (1, 123456, 255), (2**63 + 5, 2**32 - 1, 7)]:
+        out = np.empty(1000, dtype=np.float64)
+        assert dev.yart_probe_rng(0, seed, pixel, sample, 1000, out.ctypes.data_as(C.c_void_p)) == 0
+        np.testing.assert_array_equal(out, O.rng_f64(seed, pixel, sample, 1000))
+
+
+def _probe(dev, op, a, b=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    out = np.empty_like(a)
+    bp = None if b is None else np.ascontiguousarray(b, dtype=np.float64).ctypes.data_as(C.c_void_p)
+    assert dev.yart_probe_math(0, op, a.ctypes.data_as(C.c_void_p), bp, a.size, out.ctypes.data_as(C.c_void_p)) == 0
+    return out
+
+
+def test_device_sqrt_and_div_are_ieee(dev):
+    rng = np.random.default_rng(3)
+    a = np.concatenate([rng.uniform(0, 1e6, 100000), rng.uniform(0, 1e-3, 10000), 10.0 ** rng.uniform(-300, 300, 10000)])
+    b = np.concatenate([rng.uniform(-1e3, 1e3, 110000), 10.0 ** rng.uniform(-300, 300, 10000)])
+    np.testing.assert_array_equal(_probe(dev, 0, a), np.sqrt(a))
+    np.testing.assert_array_equal(_probe(dev, 1, a, b), a / b)
+
+
+def test_device_sin_cos_match_oracle(dev):
+    rng = np.random.default_rng(4)
+    a = np.concatenate([rng.uniform(0, 2 * math.pi, 50000), rng.uniform(-500, 500, 50000)])
+    L = O.lib()
+    np.testing.assert_array_equal(_probe(dev, 2, a), np.array([L.oracle_sin(x) for x in a]))
+    np.testing.assert_array_equal(_probe(dev, 3, a), np.array([L.oracle_cos(x) for x in a]))
+
+
+def _hits_equal(h1, o1, h2, o2):
+    np.testing.assert_array_equal(o1, o2)
+    m = o1 >= 0
+    np.testing.assert_array_equal(h1[m], h2[m])
+
+
+def test_intersect_qbvh_fixture(dev):
+    from test_oracle_known_answers import FIXTURE_RAY, fixture_scene
+    for rev in (False, True):
+        b = fixture_scene(rev)
+        d = b.desc()
+        s = yart.DeviceScene(d)
+        h, o = s.intersect(np.array(FIXTURE_RAY + [0.0, np.inf]))
+        assert o[0] == (2 if rev else 1)
+        assert abs(h[0, 0] - 0.954084586) < 1e-9
+        h2, o2 = O.OracleScene(d).intersect(np.array(FIXTURE_RAY + [0.0, np.inf]))
+        _hits_equal(h, o, h2, o2)
+
+
+def _random_rays(n, lo, hi, seed):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(lo, hi, (n, 3))
+    d = rng.normal(size=(n, 3))
+    r = np.concatenate([o, d, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+    return r
+
+
+@pytest.mark.parametrize("scene", ["cornell-box", "david", "sycee", "three-spheres", "random-scene"])
+def test_intersect_matches_oracle(dev, scene):
+    p = yart.Preset(scene)
+    bounds = {"cornell-box": (0, 555), "david": (-150, 250), "sycee": (-4, 4), "three-spheres": (-3, 3),
+              "random-scene": (-12, 12)}[scene]
+    rays = _random_rays(200000, *bounds, seed=11)
+    # camera-like rays too: from the preset's eye towards the scene
+    eye = np.array(p.defaults.lookfrom)
+    tgt = _random_rays(50000, *bounds, seed=12)[:, :3]
+    cam_rays = np.concatenate([np.tile(eye, (50000, 1)), tgt - eye, np.full((50000, 1), 0.001),
+                               np.full((50000, 1), np.inf)], axis=1)
+    rays = np.concatenate([rays, cam_rays])
+    s = yart.DeviceScene(p.desc)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o >= 0).mean() > 0.05
+    _hits_equal(h, o, h2, o2)
+
+
+def test_scene_info_matches_reference_qbvh(dev):
+    s = yart.DeviceScene(yart.Preset("david").desc)
+    i = s.info()
+    assert (i.bvh_nodes, i.bvh_leaves, i.bvh_max_depth) == (5461, 16384, 7)  # one shared BLAS for both instances
+    assert i.n_meshes == 1 and i.n_objects == 7 and i.n_lights == 5
+
+
+RENDER_CASES = [
+    # scene, W, H, spp, depth
+    ("cornell-box", 64, 64, 16, 50),
+    ("cornell-box", 37, 29, 5, 50),     # ragged: W, H not multiples of 8 -> uncovered crop rows/cols
+    ("two-spheres", 100, 56, 8, 8),     # C1 at reduced size (checker texture, no lights)
+    ("random-scene", 60, 40, 4, 50),    # C3 at reduced size (metal / negative albedo / glass)
+    ("three-spheres", 40, 40, 4, 50),   # negative-radius spheres
+    ("bunny", 40, 40, 4, 50),           # C4 (stand-in mesh) at reduced size
+    ("david", 48, 27, 2, 50),           # C5 at reduced size (2 mesh instances)
+    ("cornell-box", 16, 16, 3, 1),      # depth 1: every path ends at `depth == 0 -> 1.0`
+]
+
+
+@pytest.mark.parametrize("scene,W,H,spp,depth", RENDER_CASES)
+def test_render_bitwise_equal_to_oracle(dev, scene, W, H, spp, depth):
+    p = yart.Preset(scene)
+    cam = p.camera(W, H)
+    prm = yart.render_params(W, H, spp, depth)
+    gpu = yart.DeviceScene(p.desc).render(cam, prm)
+    cpu = O.OracleScene(p.desc).render(cam, prm, threads=0)
+    assert np.isfinite(gpu).all()
+    np.testing.assert_array_equal(gpu, cpu)
+    cov = O.coverage(W, H)
+    assert (gpu[~cov] == 0).all()
+    assert (gpu[cov].sum(axis=-1) != 0).mean() > 0.05
+
+
+def test_shards_partition_the_frame(dev):
+    p = yart.Preset("cornell-box")
+    W, H, spp = 72, 48, 4
+    cam = p.camera(W, H)
+    s = yart.DeviceScene(p.desc)
+    full = s.render(cam, yart.render_params(W, H, spp, 50))
+    parts = [s.render(cam, yart.render_params(W, H, spp, 50, shard_index=i, shard_count=3)) for i in range(3)]
+    nz = [(q.sum(axis=-1) != 0) for q in parts]
+    assert not (nz[0] & nz[1]).any() and not (nz[1] & nz[2]).any() and not (nz[0] & nz[2]).any()
+    np.testing.assert_array_equal(parts[0] + parts[1] + parts[2], full)
+
+
+def test_finalize_matches_oracle(dev):
+    p = yart.Preset("cornell-box")
+    W, H, spp = 96, 64, 8
+    xyz = O.OracleScene(p.desc).render(p.camera(W, H), yart.render_params(W, H, spp, 50))
+    g = yart.finalize_rgba8(xyz, spp)
+    c = O.finalize(xyz, spp)
+    diff = np.abs(g.astype(int) - c.astype(int))
+    assert diff.max() <= 1
+    assert (diff > 0).mean() <= 1e-3
+    np.testing.assert_array_equal(g[..., 3], c[..., 3])
+
+
+def test_errors_are_reported_not_raised(dev):
+    b = O.DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    b.mesh(np.zeros((3, 9), dtype=np.float32), np.zeros((3, 9)))  # <= 4 triangles: reference panics
+    b.obj(abi.PRIM_MESH, m, mesh=0)
+    with pytest.raises(yart.YartError) as e:
+        yart.DeviceScene(b.desc())
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    b2 = O.DescBuilder()
+    b2.obj(abi.PRIM_SPHERE, 3, (0, 0, 0, 1))  # material index out of range
+    with pytest.raises(yart.YartError) as e:
+        yart.DeviceScene(b2.desc())
+    assert e.value.code == abi.ERR_INVALID

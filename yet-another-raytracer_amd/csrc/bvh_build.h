@@ -1,0 +1,26 @@
+// bvh_build.h — host-side construction of the reference's 4-wide QBVH for one mesh.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "device_types.h"
+
+namespace yart_dev {
+
+struct BuiltMesh {
+  std::vector<DevNode> nodes;       // post-order; root = nodes.back()
+  std::vector<float> leaves;        // 36 floats per leaf (SoA, see DevMesh)
+  std::vector<uint32_t> leaf_first; // first sorted triangle of each leaf
+  std::vector<double> normals;      // 9 per sorted triangle
+  uint32_t depth = 0;               // inner-node levels on the deepest path
+};
+
+// L4QBVH::new (qbvh.rs:252-361): recursive median split into four children per node, <= 4
+// triangles per leaf, centroid-extent axis choice and sort (qbvh.rs:637-693). Rust's
+// sort_unstable_by leaves the order of equal keys unspecified; this build breaks ties by the
+// triangle's input index (the oracle does the same). Returns false (with `err`) when the mesh
+// cannot be traversed the way the reference does (<= 4 triangles: qbvh.rs:383-384 underflows).
+bool build_qbvh(uint32_t n_tris, const float* positions, const double* normals, BuiltMesh& out, std::string& err);
+
+}  // namespace yart_dev

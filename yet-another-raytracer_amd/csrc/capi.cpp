@@ -1,0 +1,385 @@
+// capi.cpp — the C ABI of include/yart.h: scene upload to HBM, launches, host conveniences.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/yart.h"
+#include "../host/camera_impl.h"
+#include "bvh_build.h"
+#include "kernels.h"
+
+using namespace yart_dev;
+
+namespace {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& m) { g_err = m; return code; }
+int ok() { g_err.clear(); return YART_OK; }
+int hip_fail(hipError_t e, const char* what) {
+  return fail(YART_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr, what)                      \
+  do {                                           \
+    hipError_t e_ = (expr);                      \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+// Smits basis spectra (color.rs:1711-1982): white, cyan, magenta, yellow, red, green, blue.
+const double kSmits[7][36] = {
+#include "smits.inc"
+};
+
+// RGB::into_spectrum (color.rs:54-90) at bin i; Spectrum += is `self = rhs + self` from 0.0.
+double spectrum_bin(const double rgb[3], int i) {
+  enum { W, Cy, Ma, Ye, Re, Gr, Bl };
+  const double red = rgb[0], green = rgb[1], blue = rgb[2];
+  double s = 0.0;
+  if (red <= green && red <= blue) {
+    s = red * kSmits[W][i] + s;
+    if (green <= blue) { s = (green - red) * kSmits[Cy][i] + s; s = (blue - green) * kSmits[Bl][i] + s; }
+    else { s = (blue - red) * kSmits[Cy][i] + s; s = (green - blue) * kSmits[Gr][i] + s; }
+  } else if (green <= red && green <= blue) {
+    s = green * kSmits[W][i] + s;
+    if (red <= blue) { s = (red - green) * kSmits[Ma][i] + s; s = (blue - red) * kSmits[Bl][i] + s; }
+    else { s = (blue - green) * kSmits[Ma][i] + s; s = (red - blue) * kSmits[Re][i] + s; }
+  } else {
+    s = blue * kSmits[W][i] + s;
+    if (red <= green) { s = (red - blue) * kSmits[Ye][i] + s; s = (green - red) * kSmits[Gr][i] + s; }
+    else { s = (green - blue) * kSmits[Ye][i] + s; s = (red - green) * kSmits[Re][i] + s; }
+  }
+  return s;
+}
+
+class DeviceGuard {  // keep the caller's current device (torch tracks its own)
+ public:
+  explicit DeviceGuard(int dev) { (void)hipGetDevice(&old_); if (old_ != dev) (void)hipSetDevice(dev); dev_ = dev; }
+  ~DeviceGuard() { if (old_ != dev_) (void)hipSetDevice(old_); }
+ private:
+  int old_ = 0, dev_ = 0;
+};
+
+template <class T>
+hipError_t upload(std::vector<void*>& owned, const T* src, size_t n, const T** dst, uint64_t& bytes) {
+  if (n == 0) { *dst = nullptr; return hipSuccess; }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, sizeof(T) * n);
+  if (e != hipSuccess) return e;
+  owned.push_back(p);
+  bytes += sizeof(T) * n;
+  *dst = static_cast<const T*>(p);
+  return hipMemcpy(p, src, sizeof(T) * n, hipMemcpyHostToDevice);
+}
+
+bool valid_objects(const yart_scene_desc* d, const yart_object* o, uint32_t n, bool lights, std::string& why) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (o[i].kind > YART_PRIM_MESH) { why = "object kind out of range"; return false; }
+    if (o[i].n_xforms > YART_MAX_XFORMS) { why = "too many wrappers"; return false; }
+    for (uint32_t l = 0; l < o[i].n_xforms; ++l)
+      if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_FLIP_FACE) { why = "bad wrapper kind"; return false; }
+    if (o[i].kind == YART_PRIM_MESH && o[i].mesh >= d->n_meshes) { why = "mesh index out of range"; return false; }
+    if (!lights && o[i].material >= d->n_materials) { why = "material index out of range"; return false; }
+  }
+  return true;
+}
+
+DevObject to_dev(const yart_object& o) {
+  DevObject d{};
+  d.kind = o.kind; d.material = o.material; d.mesh = o.mesh; d.n_xf = o.n_xforms;
+  for (uint32_t l = 0; l < o.n_xforms && l < (uint32_t)kMaxXforms; ++l) {
+    d.xf_kind[l] = o.xforms[l].kind;
+    if (o.xforms[l].kind == YART_XF_ROTATE_Y) {  // RotateY::new (hittable.rs:173-176)
+      const double radians = o.xforms[l].v[0] * 3.141592653589793 / 180.0;
+      d.xf[l][0] = std::sin(radians);
+      d.xf[l][1] = std::cos(radians);
+    } else {
+      for (int k = 0; k < 3; ++k) d.xf[l][k] = o.xforms[l].v[k];
+    }
+  }
+  for (int k = 0; k < 24; ++k) d.p[k] = o.p[k];
+  return d;
+}
+
+}  // namespace
+
+struct yart_scene {
+  int device = 0;
+  DevScene dev{};
+  std::vector<void*> owned;
+  yart_scene_info info{};
+  ~yart_scene() {
+    DeviceGuard g(device);
+    for (void* p : owned) (void)hipFree(p);
+  }
+};
+
+extern "C" {
+
+const char* yart_version(void) { return "yart-mi355x 0.1 (gfx950, f64 megakernel, ABI 1)"; }
+const char* yart_last_error(void) { return g_err.c_str(); }
+
+int yart_device_count(int* out) {
+  if (!out) return fail(YART_ERR_INVALID, "null argument");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) { *out = 0; return hip_fail(e, "hipGetDeviceCount"); }
+  *out = n;
+  return ok();
+}
+
+int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lookat[3], const double vup[3],
+                     double vfov, double aspect, double aperture, double focus_dist, double t0, double t1) {
+  int rc = yart_camera_init_impl(cam, lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist, t0, t1);
+  return rc ? fail(rc, "null argument") : ok();
+}
+
+int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
+  if (!d || !out) return fail(YART_ERR_INVALID, "null argument");
+  if (d->abi_version != YART_ABI_VERSION) return fail(YART_ERR_INVALID, "abi_version mismatch");
+  if ((d->n_objects && !d->objects) || (d->n_lights && !d->lights) || (d->n_materials && !d->materials) ||
+      (d->n_textures && !d->textures) || (d->n_meshes && !d->meshes))
+    return fail(YART_ERR_INVALID, "null array with non-zero count");
+  std::string why;
+  if (!valid_objects(d, d->objects, d->n_objects, false, why) || !valid_objects(d, d->lights, d->n_lights, true, why))
+    return fail(YART_ERR_INVALID, why);
+  for (uint32_t i = 0; i < d->n_materials; ++i) {
+    const yart_material& m = d->materials[i];
+    if (m.kind > YART_MAT_DIFFUSE_LIGHT) return fail(YART_ERR_INVALID, "material kind out of range");
+    bool textured = m.kind == YART_MAT_LAMBERTIAN || m.kind == YART_MAT_METAL || m.kind == YART_MAT_DIFFUSE_LIGHT;
+    if (textured && m.texture >= d->n_textures) return fail(YART_ERR_INVALID, "texture index out of range");
+  }
+  for (uint32_t i = 0; i < d->n_textures; ++i)
+    if (d->textures[i].kind > YART_TEX_CHECKER) return fail(YART_ERR_INVALID, "texture kind out of range");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return fail(YART_ERR_INVALID, "device index out of range");
+
+  // host-side preparation (no device work yet)
+  std::vector<DevObject> objs, lights;
+  for (uint32_t i = 0; i < d->n_objects; ++i) objs.push_back(to_dev(d->objects[i]));
+  for (uint32_t i = 0; i < d->n_lights; ++i) lights.push_back(to_dev(d->lights[i]));
+  std::vector<DevMaterial> mats(d->n_materials);
+  for (uint32_t i = 0; i < d->n_materials; ++i) {
+    const yart_material& m = d->materials[i];
+    mats[i].kind = m.kind; mats[i].texture = m.texture; mats[i].fuzz = m.fuzz;
+    for (int k = 0; k < 3; ++k) { mats[i].b[k] = m.b[k]; mats[i].c[k] = m.c[k]; }
+  }
+  std::vector<DevTexture> texs(d->n_textures);
+  for (uint32_t i = 0; i < d->n_textures; ++i) {
+    const yart_texture& t = d->textures[i];
+    texs[i].kind = t.kind;
+    for (int b = 0; b < kBins; ++b) {
+      texs[i].spec[b] = spectrum_bin(t.rgb, b);
+      texs[i].spec_even[b] = t.kind == YART_TEX_CHECKER ? spectrum_bin(t.rgb_even, b) : 0.0;
+    }
+  }
+  double bg[kBins];
+  for (int b = 0; b < kBins; ++b) bg[b] = spectrum_bin(d->background, b);
+  std::vector<BuiltMesh> built(d->n_meshes);
+  uint32_t nodes = 0, leaves = 0, depth = 0;
+  for (uint32_t m = 0; m < d->n_meshes; ++m) {
+    const yart_mesh& ym = d->meshes[m];
+    if (!ym.positions || !ym.normals) return fail(YART_ERR_INVALID, "mesh without positions/normals");
+    std::string err;
+    if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err)) return fail(YART_ERR_UNSUPPORTED, err);
+    nodes += (uint32_t)built[m].nodes.size();
+    leaves += (uint32_t)built[m].leaf_first.size();
+    depth = std::max(depth, built[m].depth);
+  }
+
+  auto s = std::make_unique<yart_scene>();
+  s->device = device;
+  DeviceGuard guard(device);
+  uint64_t bytes = 0;
+  DevScene& ds = s->dev;
+  HIP_TRY(upload(s->owned, objs.data(), objs.size(), &ds.objects, bytes), "upload objects");
+  HIP_TRY(upload(s->owned, lights.data(), lights.size(), &ds.lights, bytes), "upload lights");
+  HIP_TRY(upload(s->owned, mats.data(), mats.size(), &ds.materials, bytes), "upload materials");
+  HIP_TRY(upload(s->owned, texs.data(), texs.size(), &ds.textures, bytes), "upload textures");
+  HIP_TRY(upload(s->owned, bg, kBins, &ds.background, bytes), "upload background");
+  std::vector<DevMesh> dm(d->n_meshes);
+  for (uint32_t m = 0; m < d->n_meshes; ++m) {
+    BuiltMesh& b = built[m];
+    HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
+    HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
+    HIP_TRY(upload(s->owned, b.leaf_first.data(), b.leaf_first.size(), &dm[m].leaf_first, bytes), "upload leaf_first");
+    HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
+    dm[m].root = (uint32_t)b.nodes.size() - 1;
+    dm[m].n_nodes = (uint32_t)b.nodes.size();
+  }
+  HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
+  ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
+  ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
+  ds.has_mesh = 0;
+  for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
+
+  yart_scene_info& in = s->info;
+  in.device = device; in.n_objects = d->n_objects; in.n_lights = d->n_lights; in.n_meshes = d->n_meshes;
+  in.bvh_nodes = nodes; in.bvh_leaves = leaves; in.bvh_max_depth = depth;
+  in.bvh_max_stack = d->n_meshes ? 3 * depth + 1 : 0;
+  in.device_bytes = bytes;
+  *out = s.release();
+  return ok();
+}
+
+void yart_scene_destroy(yart_scene* s) { delete s; }
+
+int yart_scene_get_info(const yart_scene* s, yart_scene_info* out) {
+  if (!s || !out) return fail(YART_ERR_INVALID, "null argument");
+  *out = s->info;
+  return ok();
+}
+
+static int make_args(const yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* out,
+                     RenderArgs& a) {
+  if (!s || !cam || !p) return fail(YART_ERR_INVALID, "null argument");
+  if (p->width == 0 || p->height == 0) return fail(YART_ERR_INVALID, "width and height must be > 0");
+  if ((uint64_t)p->width * p->height > 0xFFFFFFFFull) return fail(YART_ERR_INVALID, "image too large (pixel index is 32-bit)");
+  const uint32_t sc = p->shard_count ? p->shard_count : 1;
+  if (p->shard_index >= sc) return fail(YART_ERR_INVALID, "shard_index >= shard_count");
+  a.cam = *cam;
+  a.width = p->width; a.height = p->height; a.spp = p->spp; a.max_depth = p->max_depth; a.seed = p->seed;
+  a.shard_index = p->shard_index; a.shard_count = sc;
+  a.blocks_x = (p->width + 7) / 8;
+  const uint32_t total = a.blocks_x * ((p->height + 7) / 8);
+  a.n_blocks = total > p->shard_index ? (total - p->shard_index + sc - 1) / sc : 0;
+  a.out = out;
+  a.stats = nullptr;
+  return YART_OK;
+}
+
+int yart_render_async(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* d_xyz_sum,
+                      void* stream) {
+  RenderArgs a;
+  if (int rc = make_args(s, cam, p, d_xyz_sum, a)) return rc;
+  if (!d_xyz_sum) return fail(YART_ERR_INVALID, "null output");
+  DeviceGuard g(s->device);
+  HIP_TRY(launch_render(s->dev, a, false, (hipStream_t)stream), "launch k_render");
+  return ok();
+}
+
+static int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* host_out,
+                       yart_render_stats* stats) {
+  RenderArgs a;
+  if (int rc = make_args(s, cam, p, nullptr, a)) return rc;
+  if (!host_out) return fail(YART_ERR_INVALID, "null output");
+  DeviceGuard g(s->device);
+  const size_t bytes = sizeof(double) * 3 * (size_t)p->width * p->height;
+  double* d_out = nullptr;
+  unsigned long long* d_stats = nullptr;
+  HIP_TRY(hipMalloc(&d_out, bytes), "hipMalloc output");
+  std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
+  HIP_TRY(hipMemset(d_out, 0, bytes), "hipMemset");
+  if (stats) {
+    HIP_TRY(hipMalloc(&d_stats, 8 * sizeof(unsigned long long)), "hipMalloc stats");
+    HIP_TRY(hipMemset(d_stats, 0, 8 * sizeof(unsigned long long)), "hipMemset");
+  }
+  std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
+  a.out = d_out;
+  a.stats = d_stats;
+  HIP_TRY(launch_render(s->dev, a, stats != nullptr, nullptr), "launch k_render");
+  HIP_TRY(hipDeviceSynchronize(), "k_render");
+  HIP_TRY(hipMemcpy(host_out, d_out, bytes, hipMemcpyDeviceToHost), "copy output");
+  if (stats) {
+    unsigned long long v[8];
+    HIP_TRY(hipMemcpy(v, d_stats, sizeof v, hipMemcpyDeviceToHost), "copy stats");
+    std::memset(stats, 0, sizeof *stats);
+    stats->samples = v[0]; stats->segments = v[1]; stats->prim_tests = v[2]; stats->node_visits = v[3];
+    stats->leaf_visits = v[4]; stats->leaf_tris = v[5]; stats->light_tests = v[6];
+  }
+  return ok();
+}
+
+int yart_render(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* xyz_sum_out,
+                yart_progress_fn progress, void* user) {
+  int rc = render_host(s, cam, p, xyz_sum_out, nullptr);
+  if (rc == YART_OK && progress) progress((uint64_t)p->width * p->height, user);
+  return rc;
+}
+
+int yart_render_with_stats(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* xyz_sum_out,
+                           yart_render_stats* stats) {
+  if (!stats) return fail(YART_ERR_INVALID, "null stats");
+  return render_host(s, cam, p, xyz_sum_out, stats);
+}
+
+int yart_finalize_rgba8_async(int device, const double* d_xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* d_rgba,
+                              void* stream) {
+  if (!d_xyz || !d_rgba || !w || !h) return fail(YART_ERR_INVALID, "bad argument");
+  DeviceGuard g(device);
+  HIP_TRY(launch_finalize(d_xyz, w, h, spp, d_rgba, (hipStream_t)stream), "launch k_finalize");
+  return ok();
+}
+
+int yart_finalize_rgba8(int device, const double* xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba) {
+  if (!xyz || !rgba || !w || !h) return fail(YART_ERR_INVALID, "bad argument");
+  DeviceGuard g(device);
+  const size_t n = (size_t)w * h;
+  double* dx = nullptr;
+  uint8_t* dr = nullptr;
+  HIP_TRY(hipMalloc(&dx, sizeof(double) * 3 * n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h1(dx, &hipFree);
+  HIP_TRY(hipMalloc(&dr, 4 * n), "hipMalloc");
+  std::unique_ptr<uint8_t, decltype(&hipFree)> h2(dr, &hipFree);
+  HIP_TRY(hipMemcpy(dx, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice), "copy in");
+  HIP_TRY(launch_finalize(dx, w, h, spp, dr, nullptr), "launch k_finalize");
+  HIP_TRY(hipDeviceSynchronize(), "k_finalize");
+  HIP_TRY(hipMemcpy(rgba, dr, 4 * n, hipMemcpyDeviceToHost), "copy out");
+  return ok();
+}
+
+int yart_intersect(yart_scene* s, const double* rays, uint32_t n, double* hits, int32_t* obj) {
+  if (!s || (n && (!rays || !hits || !obj))) return fail(YART_ERR_INVALID, "null argument");
+  if (n == 0) return ok();
+  DeviceGuard g(s->device);
+  double *dr = nullptr, *dh = nullptr;
+  int32_t* dobj = nullptr;
+  HIP_TRY(hipMalloc(&dr, sizeof(double) * 8 * (size_t)n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h1(dr, &hipFree);
+  HIP_TRY(hipMalloc(&dh, sizeof(double) * 8 * (size_t)n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h2(dh, &hipFree);
+  HIP_TRY(hipMalloc(&dobj, sizeof(int32_t) * (size_t)n), "hipMalloc");
+  std::unique_ptr<int32_t, decltype(&hipFree)> h3(dobj, &hipFree);
+  HIP_TRY(hipMemcpy(dr, rays, sizeof(double) * 8 * (size_t)n, hipMemcpyHostToDevice), "copy rays");
+  HIP_TRY(launch_intersect(s->dev, dr, n, dh, dobj, nullptr), "launch k_intersect");
+  HIP_TRY(hipDeviceSynchronize(), "k_intersect");
+  HIP_TRY(hipMemcpy(hits, dh, sizeof(double) * 8 * (size_t)n, hipMemcpyDeviceToHost), "copy hits");
+  HIP_TRY(hipMemcpy(obj, dobj, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost), "copy obj");
+  return ok();
+}
+
+int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, double* out) {
+  if (!out || n == 0) return fail(YART_ERR_INVALID, "bad argument");
+  DeviceGuard g(device);
+  double* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(double) * n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h(d, &hipFree);
+  HIP_TRY(launch_probe_rng(seed, pixel, sample, n, d, nullptr), "launch k_probe_rng");
+  HIP_TRY(hipDeviceSynchronize(), "k_probe_rng");
+  HIP_TRY(hipMemcpy(out, d, sizeof(double) * n, hipMemcpyDeviceToHost), "copy");
+  return ok();
+}
+
+int yart_probe_math(int device, int op, const double* a, const double* b, uint32_t n, double* out) {
+  if (!a || !out || n == 0 || ((op == 1 || op == 4) && !b)) return fail(YART_ERR_INVALID, "bad argument");
+  DeviceGuard g(device);
+  double *da = nullptr, *db = nullptr, *dout = nullptr;
+  HIP_TRY(hipMalloc(&da, sizeof(double) * n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h1(da, &hipFree);
+  HIP_TRY(hipMalloc(&db, sizeof(double) * n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h2(db, &hipFree);
+  HIP_TRY(hipMalloc(&dout, sizeof(double) * n), "hipMalloc");
+  std::unique_ptr<double, decltype(&hipFree)> h3(dout, &hipFree);
+  HIP_TRY(hipMemcpy(da, a, sizeof(double) * n, hipMemcpyHostToDevice), "copy a");
+  HIP_TRY(hipMemcpy(db, b ? b : a, sizeof(double) * n, hipMemcpyHostToDevice), "copy b");
+  HIP_TRY(launch_probe_math(op, da, db, n, dout, nullptr), "launch k_probe_math");
+  HIP_TRY(hipDeviceSynchronize(), "k_probe_math");
+  HIP_TRY(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost), "copy out");
+  return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,73 @@
+// device_types.h — HBM layout of a scene on one MI355X (shared by the host side of libyart and
+// the kernels). Everything the per-sample loop reads is resident; nothing is rebuilt per frame.
+//
+//  DevObject   world / light list entries in list order (hittable.rs:47-123). 320 B each; a wave
+//              walks the list with a wave-uniform index, so the fields come in on the scalar path.
+//  DevMaterial material table (material.rs), 64 B.
+//  DevTexture  36-bin spectra precomputed from RGB with the Smits basis (color.rs:54-90): the
+//              reference recomputes the whole spectrum per lookup and reads one bin; the bins are
+//              bitwise the values it would read.
+//  Mesh BLAS   the reference's L4QBVH (qbvh.rs:244-600) with its exact topology and child order:
+//              DevNode 128 B (6 x float4 of child boxes, 4 child ids, axes); leaves as 144-B
+//              SoA blocks of <= 4 triangles (9 x float4: v0 v1 v2 x/y/z per lane) + the f64
+//              interpolated-normal table. Every f32 here is exact: tobj parses positions as f32
+//              (triangle.rs:438) and box corners are min/max of those, so the f64 arithmetic of
+//              the reference is reproduced bit for bit by converting on load.
+#pragma once
+#include <stdint.h>
+
+namespace yart_dev {
+
+constexpr int kMaxXforms = 4;
+constexpr int kBins = 36;
+constexpr int kStackSlots = 32;  // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
+
+struct DevObject {
+  uint32_t kind, material, mesh, n_xf;
+  uint32_t xf_kind[kMaxXforms];
+  double xf[kMaxXforms][3];  // TRANSLATE: offset; ROTATE_Y: sin, cos (hittable.rs:173-176)
+  double p[24];
+};
+
+struct DevMaterial {
+  uint32_t kind, texture;
+  double fuzz;
+  double b[3], c[3];
+};
+
+struct DevTexture {
+  uint32_t kind, reserved;
+  double spec[kBins];       // SOLID / CHECKER odd
+  double spec_even[kBins];  // CHECKER even
+};
+
+struct alignas(16) DevNode {
+  float bmin[3][4];   // [axis][child]
+  float bmax[3][4];
+  uint32_t child[4];  // inner: node index; leaf: 1<<31 | count<<27 | leaf index
+  uint32_t axes;      // top | left << 2 | right << 4
+  uint32_t pad[3];
+};
+static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
+
+struct DevMesh {
+  const DevNode* nodes;
+  const float* leaves;        // 36 floats per leaf: [v0x v0y v0z v1x v1y v1z v2x v2y v2z][4 lanes]
+  const uint32_t* leaf_first; // first (sorted) triangle index of each leaf
+  const double* normals;      // 9 per sorted triangle: n0 n1 n2
+  uint32_t root;              // the last node pushed (qbvh.rs:384)
+  uint32_t n_nodes;
+};
+
+struct DevScene {
+  const DevObject* objects;
+  const DevObject* lights;
+  const DevMaterial* materials;
+  const DevTexture* textures;
+  const DevMesh* meshes;
+  const double* background;  // 36 bins
+  uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
+  uint32_t has_mesh;
+};
+
+}  // namespace yart_dev

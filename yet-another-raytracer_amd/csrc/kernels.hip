@@ -1,0 +1,799 @@
+// kernels.hip — gfx950 kernels of the path-tracing hot path.
+//
+// k_render is a persistent-lane megakernel: one wave64 owns one 8x8 pixel block, one lane owns
+// one pixel, and each lane runs its pixel's samples back to back with the sample loop and the
+// bounce loop fused into a single `while (alive)` (main.rs:690-708 around ray_reflectance,
+// main.rs:537-588, unrolled front to back). A lane whose path ends starts its next sample on the
+// next iteration, so the wave stays full until its pixels run out of samples: ray compaction
+// without a queue, and per-pixel sums in sample order (bitwise the CPU restatement's).
+//
+// Arithmetic is IEEE f64 like the reference (built with -ffp-contract=off, so no operation is
+// fused); the expression order of every function follows the Rust source it cites. The scene's
+// world list is walked with a wave-uniform index (the objects arrive on the scalar path); the
+// mesh QBVH is traversed per lane with a 32-slot stack in LDS laid out [slot][lane] so every
+// stack access is bank-conflict free.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "kernels.h"
+
+namespace yart_dev {
+
+// ------------------------------------------------------------------------ tables / constants
+__constant__ double c_cie[471][3] = {  // color.rs:286-1709, rows (x, y, z) per nm from 360
+#include "cie_xyz.inc"
+};
+constexpr double kMinLambda = 360.0, kMaxLambda = 720.0, kBinWidth = 10.0;  // color.rs:7-9
+constexpr double kCieYIntegral = 106.856895;                               // color.rs:12
+constexpr double kMaxLum = 20.0;                                            // main.rs:59
+constexpr double kPi = 3.141592653589793;
+constexpr double kEps = 2.220446049250313e-16;                              // f64::EPSILON
+constexpr double kF64Max = 1.7976931348623157e308;
+
+// ---------------------------------------------------------------------- Vec3 (vec3.rs)
+struct V3 { double x, y, z; };
+__device__ __forceinline__ V3 mk(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 muls(V3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 smul(double s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 divs(V3 a, double s) {  // vec3.rs:109-122 (0 -> f64::MAX)
+  if (s == 0.0) return mk(kF64Max, kF64Max, kF64Max);
+  return mk(a.x / s, a.y / s, a.z / s);
+}
+__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ V3 unit(V3 a) { double l = len(a); return mk(a.x / l, a.y / l, a.z / l); }
+__device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
+
+struct Ray { V3 o, d; double time, wl; };
+__device__ __forceinline__ V3 at(const Ray& r, double t) { return add(r.o, smul(t, r.d)); }
+
+struct Hit { double t; V3 p, n; bool ff; uint32_t mat; };
+
+// ------------------------------------------------- deterministic sin/cos (oracle.c twin)
+__device__ __forceinline__ void rem_pio2(double x, int& q, double& y0, double& y1) {
+  const double INV_PIO2 = 6.36619772367581382433e-01, PIO2_1 = 1.57079632673412561417e+00,
+               PIO2_2 = 6.07710050630396597660e-11, PIO2_2T = 2.02226624879595063154e-21;
+  double fn = floor(x * INV_PIO2 + 0.5);
+  double t = x - fn * PIO2_1;
+  double w = fn * PIO2_2;
+  double r = t - w;
+  w = fn * PIO2_2T - ((t - r) - w);
+  y0 = r - w;
+  y1 = (r - y0) - w;
+  q = (int)((long long)fn & 3);
+}
+__device__ __forceinline__ double k_sin(double x, double y) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  double z = x * x, v = z * x;
+  double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+__device__ __forceinline__ double k_cos(double x, double y) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  double z = x * x;
+  double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+  double hz = 0.5 * z, w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+__device__ __forceinline__ void sincos_det(double x, double& s, double& c) {
+  int q; double y0, y1;
+  rem_pio2(x, q, y0, y1);
+  double ks = k_sin(y0, y1), kc = k_cos(y0, y1);
+  s = (q == 0) ? ks : (q == 1) ? kc : (q == 2) ? -ks : -kc;
+  c = (q == 0) ? kc : (q == 1) ? -ks : (q == 2) ? -kc : ks;
+}
+__device__ __forceinline__ double sin_det(double x) { double s, c; sincos_det(x, s, c); return s; }
+__device__ __forceinline__ double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }  // material.rs:210
+
+// ---------------------------------------------------------------- RNG (Philox4x32-10)
+struct Rng { uint32_t k0, k1, c0, c1, c2, c3, b0, b1, b2, b3; int have; };
+__device__ __forceinline__ void rng_init(Rng& r, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
+  r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32);
+  r.c0 = 0; r.c1 = sample; r.c2 = pixel; r.c3 = stream; r.have = 0;
+}
+__device__ __forceinline__ void philox(Rng& r) {
+  uint32_t c0 = r.c0, c1 = r.c1, c2 = r.c2, c3 = r.c3, k0 = r.k0, k1 = r.k1;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  r.b0 = c0; r.b1 = c1; r.b2 = c2; r.b3 = c3;
+}
+__device__ __forceinline__ uint64_t rng_u64(Rng& r) {
+  if (r.have == 0) { philox(r); r.c0++; r.have = 2; }
+  uint64_t v = (r.have == 2) ? (((uint64_t)r.b1 << 32) | r.b0) : (((uint64_t)r.b3 << 32) | r.b2);
+  r.have--;
+  return v;
+}
+__device__ __forceinline__ double gen_f64(Rng& r) { return (double)(rng_u64(r) >> 11) * 0x1.0p-53; }
+__device__ __forceinline__ double gen_range(Rng& r, double low, double high) {  // rand 0.8.5 sample_single
+  double scale = high - low;
+  for (int guard = 0; guard < 64; ++guard) {
+    uint64_t bits = (rng_u64(r) >> 12) | 0x3FF0000000000000ull;
+    double res = (__longlong_as_double((long long)bits) - 1.0) * scale + low;
+    if (res < high) return res;
+    scale = __longlong_as_double(__double_as_longlong(scale) - 1);
+  }
+  return low;
+}
+__device__ __forceinline__ uint64_t gen_index(Rng& r, uint64_t n) {  // UniformInt<usize> 0..n
+  uint64_t zone = (n << __clzll(n)) - 1;
+  for (int guard = 0; guard < 64; ++guard) {
+    uint64_t v = rng_u64(r);
+    uint64_t hi = __umul64hi(v, n), lo = v * n;
+    if (lo <= zone) return hi;
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- spectra
+__device__ __forceinline__ int spectrum_bin(double wl) {  // color.rs:276-283
+  double f = (wl - kMinLambda) / kBinWidth;
+  if (!(f > 0.0)) return 0;
+  if (f >= 36.0) return 35;
+  return (int)f;
+}
+__device__ __forceinline__ void cie_xyz(double wl, double& x, double& y, double& z) {  // color.rs:216-228
+  double f = wl - kMinLambda;
+  if (f != f) f = 0.0;                                             // NaN as isize = 0
+  if (!(f > -1.0) || !(f < 471.0)) { x = y = z = 0.0; return; }  // (f as isize) outside 0..471
+  int i = (int)f;
+  x = c_cie[i][0]; y = c_cie[i][1]; z = c_cie[i][2];
+}
+
+// ------------------------------------------------------------------- primitive hits
+__device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // sphere.rs:48-86
+  V3 center = mk(p[0], p[1], p[2]);
+  double radius = p[3];
+  V3 oc = sub(r.o, center);
+  double a = len2(r.d);
+  double half_b = dot(oc, r.d);
+  double c = len2(oc) - radius * radius;
+  double disc = half_b * half_b - a * c;
+  if (disc < 0.0) return false;
+  double sq = sqrt(disc);
+  double t = (0.0 - half_b - sq) / a;
+  if (t < tmin || tmax < t) {
+    t = (0.0 - half_b + sq) / a;
+    if (t < tmin || tmax < t) return false;
+  }
+  V3 pt = at(r, t);
+  V3 outward = divs(sub(pt, center), fabs(radius));
+  if (radius < 0.0) { h.n = neg(outward); h.ff = dot(r.d, outward) > 0.0; }
+  else { h.n = outward; h.ff = dot(r.d, outward) < 0.0; }
+  h.t = t; h.p = pt;
+  return true;
+}
+
+// aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
+template <int A, int B, int CC>
+__device__ __forceinline__ bool rect_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
+  const double* o = &r.o.x;
+  const double* d = &r.d.x;
+  double t = (p[4] - o[A]) / d[A];
+  if (t < tmin || t > tmax) return false;
+  double x = o[B] + t * d[B];
+  double y = o[CC] + t * d[CC];
+  if (x < p[0] || x > p[1] || y < p[2] || y > p[3]) return false;
+  V3 outward = mk(A == 0 ? 1.0 : 0.0, A == 1 ? 1.0 : 0.0, A == 2 ? 1.0 : 0.0);
+  h.t = t; h.p = at(r, t);
+  if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
+  else { h.n = neg(outward); h.ff = false; }
+  return true;
+}
+__device__ __forceinline__ bool xy_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<2, 0, 1>(p, r, a, b, h); }
+__device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<1, 0, 2>(p, r, a, b, h); }
+__device__ __forceinline__ bool yz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<0, 1, 2>(p, r, a, b, h); }
+
+__device__ __forceinline__ bool box_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // box_entity.rs:53-70
+  bool found = false;
+  double closest = tmax;
+  Hit tmp;
+  double s[5];
+  s[0] = p[0]; s[1] = p[3]; s[2] = p[1]; s[3] = p[4];
+  s[4] = p[2]; if (xy_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[5]; if (xy_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[2] = p[2]; s[3] = p[5];
+  s[4] = p[1]; if (xz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[4]; if (xz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[0] = p[1]; s[1] = p[4];
+  s[4] = p[0]; if (yz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[3]; if (yz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  return found;
+}
+
+__device__ __forceinline__ bool triangle_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // triangle.rs:48-101
+  V3 v0 = ld3(p), v1 = ld3(p + 3), v2 = ld3(p + 6);
+  V3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+  V3 hh = cross(r.d, e2);
+  double a = dot(e1, hh);
+  if (a > -kEps && a < kEps) return false;
+  double f = 1.0 / a;
+  V3 s = sub(r.o, v0);
+  double u = f * dot(s, hh);
+  if (u < 0.0 || u > 1.0) return false;
+  V3 q = cross(s, e1);
+  double v = f * dot(r.d, q);
+  if (v < 0.0 || u + v > 1.0) return false;
+  double t = f * dot(e2, q);
+  if (t < tmin || t > tmax) return false;
+  double w = 1.0 - u - v;
+  V3 outward = add(add(muls(ld3(p + 9), w), muls(ld3(p + 12), u)), muls(ld3(p + 15), v));
+  h.t = t; h.p = at(r, t);
+  if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
+  else { h.n = neg(outward); h.ff = false; }
+  return true;
+}
+
+// --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543), per lane
+struct Stats { unsigned long long v[8]; };
+enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };
+
+template <bool STATS>
+__device__ __noinline__ bool qbvh_hit(const DevMesh& M, const Ray& r, double tmin, double tmax, Hit& h,
+                                      uint32_t* __restrict__ stk, Stats& st) {
+  // ORDER_TABLE (qbvh.rs:14-16), two 16-bit entries per nibble group packed in 64-bit words.
+  const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
+  const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+  const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};
+  const uint32_t pos = (rd[0] >= 0.0 ? 1u : 0u) | (rd[1] >= 0.0 ? 2u : 0u) | (rd[2] >= 0.0 ? 4u : 0u);
+  bool found = false;
+  int cursor = 0;
+  stk[0] = M.root;
+  for (;;) {
+    const uint32_t id = stk[cursor * 64];
+    if (id >> 31) {
+      const uint32_t count = (id >> 27) & 0xFu, li = id & ((1u << 27) - 1u);
+      const float4* L = reinterpret_cast<const float4*>(M.leaves + 36 * (size_t)li);
+      const float4 q0 = L[0], q1 = L[1], q2 = L[2], q3 = L[3], q4 = L[4], q5 = L[5], q6 = L[6], q7 = L[7], q8 = L[8];
+      const float lanes[9][4] = {{q0.x, q0.y, q0.z, q0.w}, {q1.x, q1.y, q1.z, q1.w}, {q2.x, q2.y, q2.z, q2.w},
+                                 {q3.x, q3.y, q3.z, q3.w}, {q4.x, q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z, q5.w},
+                                 {q6.x, q6.y, q6.z, q6.w}, {q7.x, q7.y, q7.z, q7.w}, {q8.x, q8.y, q8.z, q8.w}};
+      if (STATS) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        if (i >= count) break;
+        const double v0x = lanes[0][i], v0y = lanes[1][i], v0z = lanes[2][i];
+        const double e1x = (double)lanes[3][i] - v0x, e1y = (double)lanes[4][i] - v0y, e1z = (double)lanes[5][i] - v0z;
+        const double e2x = (double)lanes[6][i] - v0x, e2y = (double)lanes[7][i] - v0y, e2z = (double)lanes[8][i] - v0z;
+        const double hx = rd[1] * e2z - rd[2] * e2y, hy = rd[2] * e2x - rd[0] * e2z, hz = rd[0] * e2y - rd[1] * e2x;
+        const double a = e1x * hx + e1y * hy + e1z * hz;
+        const double f = 1.0 / a;
+        const double sx = ro[0] - v0x, sy = ro[1] - v0y, sz = ro[2] - v0z;
+        const double u = f * (sx * hx + sy * hy + sz * hz);
+        const double qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
+        const double v = f * (rd[0] * qx + rd[1] * qy + rd[2] * qz);
+        const double t = f * (e2x * qx + e2y * qy + e2z * qz);
+        // hitx4 (a, u, v, t range against the t_max at leaf entry) && t_max > t (strict): the
+        // current t_max never exceeds the entry value, so the strict test subsumes `t <= t_max`.
+        const bool hit = !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 &&
+                         t >= tmin && tmax > t;
+        if (hit) {
+          const double w = 1.0 - u - v;
+          const double* nn = M.normals + 9 * (size_t)(M.leaf_first[li] + i);
+          const double onx = nn[0] * w + nn[3] * u + nn[6] * v;
+          const double ony = nn[1] * w + nn[4] * u + nn[7] * v;
+          const double onz = nn[2] * w + nn[5] * u + nn[8] * v;
+          const bool ff = (rd[0] * onx + rd[1] * ony + rd[2] * onz) <= 0.0;
+          const double sign = ff ? 1.0 : -1.0;
+          tmax = t;
+          h.t = t;
+          h.p = mk(ro[0] + t * rd[0], ro[1] + t * rd[1], ro[2] + t * rd[2]);
+          h.n = mk(sign * onx, sign * ony, sign * onz);
+          h.ff = ff;
+          found = true;
+        }
+      }
+    } else {
+      const float4* N = reinterpret_cast<const float4*>(M.nodes + id);
+      const float4 mnx = N[0], mny = N[1], mnz = N[2], mxx = N[3], mxy = N[4], mxz = N[5];
+      const uint4 ch = reinterpret_cast<const uint4*>(N)[6];
+      const uint32_t axes = reinterpret_cast<const uint32_t*>(N)[28];
+      if (STATS) st.v[ST_NODES]++;
+      const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
+      const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
+      bool hk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double lo = tmin, hi = tmax;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double t0 = ((double)bmn[j][k] - ro[j]) * inv[j];
+          const double t1 = ((double)bmx[j][k] - ro[j]) * inv[j];
+          lo = fmax(lo, fmin(t0, t1));
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double t0 = ((double)bmn[j][k] - ro[j]) * inv[j];
+          const double t1 = ((double)bmx[j][k] - ro[j]) * inv[j];
+          hi = fmin(hi, fmax(t0, t1));
+        }
+        hk[k] = hi > lo;
+      }
+      const uint32_t top = axes & 3u, left = (axes >> 2) & 3u, right = (axes >> 4) & 3u;
+      const uint32_t idx = 4u * ((pos >> top) & 1u) + 2u * ((pos >> left) & 1u) + ((pos >> right) & 1u);
+      const uint32_t enc = (uint32_t)(((idx < 4 ? ORDER_LO : ORDER_HI) >> (16u * (idx & 3u))) & 0xFFFFu);
+      const uint32_t chs[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // push_hit_children (qbvh.rs:18-31)
+        const uint32_t i = (enc >> (4 * k)) & 0xFu;
+        const bool hi = (i == 0) ? hk[0] : (i == 1) ? hk[1] : (i == 2) ? hk[2] : hk[3];
+        const uint32_t c = (i == 0) ? chs[0] : (i == 1) ? chs[1] : (i == 2) ? chs[2] : chs[3];
+        if (hi) { stk[cursor * 64] = c; cursor++; }
+      }
+    }
+    if (cursor == 0) break;
+    cursor -= 1;
+  }
+  return found;
+}
+
+// ------------------------------------------------------------------------ world hit
+template <bool HAS_MESH, bool STATS>
+__device__ __forceinline__ bool prim_hit(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
+                                         double tmin, double tmax, Hit& h, uint32_t* stk, Stats& st) {
+  switch (kind) {
+    case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return xy_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return xz_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return yz_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_MESH:
+      if constexpr (HAS_MESH) return qbvh_hit<STATS>(S.meshes[o.mesh], r, tmin, tmax, h, stk, st);
+      return false;
+  }
+  return false;
+}
+
+// HittableList::hit (hittable.rs:67-79) with each entry's wrappers applied outermost first on
+// the way in (Translate :136-152, RotateY :217-251) and innermost first on the way out.
+template <bool HAS_MESH, bool STATS>
+__device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
+                                          int32_t& which, uint32_t* stk, Stats& st) {
+  bool found = false;
+  double closest = tmax;
+  for (uint32_t i = 0; i < S.n_objects; ++i) {
+    const DevObject& o = S.objects[i];
+    const uint32_t kind = o.kind, nxf = o.n_xf;
+    Ray lr = r;
+    for (uint32_t l = 0; l < nxf; ++l) {
+      const uint32_t k = o.xf_kind[l];
+      if (k == YART_XF_TRANSLATE) {
+        lr.o = sub(lr.o, ld3(o.xf[l]));
+      } else if (k == YART_XF_ROTATE_Y) {
+        const double sn = o.xf[l][0], cs = o.xf[l][1];
+        const V3 ro = lr.o, rdd = lr.d;
+        lr.o.x = cs * ro.x - sn * ro.z;
+        lr.o.z = sn * ro.x + cs * ro.z;
+        lr.d.x = cs * rdd.x - sn * rdd.z;
+        lr.d.z = sn * rdd.x + cs * rdd.z;
+      }
+    }
+    Hit t;
+    if (prim_hit<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, stk, st)) {
+      for (int l = (int)nxf - 1; l >= 0; --l) {
+        const uint32_t k = o.xf_kind[l];
+        if (k == YART_XF_TRANSLATE) {
+          t.p = add(t.p, ld3(o.xf[l]));
+        } else if (k == YART_XF_ROTATE_Y) {
+          const double sn = o.xf[l][0], cs = o.xf[l][1];
+          const V3 p = t.p, n = t.n;
+          t.p.x = cs * p.x + sn * p.z;
+          t.p.z = -sn * p.x + cs * p.z;
+          t.n.x = cs * n.x + sn * n.z;
+          t.n.z = -sn * n.x + cs * n.z;
+        } else {
+          t.ff = !t.ff;  // FlipFace (hittable.rs:338-349)
+        }
+      }
+      closest = t.t;
+      t.mat = o.material;
+      rec = t;
+      which = (int32_t)i;
+      found = true;
+    }
+  }
+  return found;
+}
+
+// ----------------------------------------------------------------------- ONB and PDFs
+struct Onb { V3 u, v, w; };
+__device__ __forceinline__ Onb onb_from_w(V3 n) {  // onb.rs:10-21
+  Onb b;
+  b.w = unit(n);
+  const V3 a = fabs(b.w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+  b.v = unit(cross(b.w, a));
+  b.u = cross(b.w, b.v);
+  return b;
+}
+__device__ __forceinline__ V3 local(const Onb& b, V3 a) { return add(add(smul(a.x, b.u), smul(a.y, b.v)), smul(a.z, b.w)); }
+__device__ __forceinline__ V3 random_cosine_direction(Rng& g) {  // pdf.rs:15-25
+  const double r1 = gen_f64(g), r2 = gen_f64(g);
+  const double z = sqrt(1.0 - r2);
+  double s, c;
+  sincos_det(2.0 * kPi * r1, s, c);
+  return mk(c * sqrt(r2), s * sqrt(r2), z);
+}
+__device__ __forceinline__ double cosine_value(const Onb& b, V3 d) {  // pdf.rs:40-47
+  const double cosine = dot(unit(d), b.w);
+  return cosine <= 0.0 ? 0.0 : cosine / kPi;
+}
+
+template <bool STATS>
+__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st) {
+  if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
+  Ray r{origin, dir, 0.0, wl};
+  Hit h;
+  if (o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:148-162
+    if (STATS) st.v[ST_LIGHT]++;
+    if (!xz_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
+    const double area = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
+    const double distance_squared = h.t * h.t * len2(dir);
+    const double cosine = fabs(dot(dir, h.n)) / len(dir);
+    return distance_squared / (cosine * area);
+  }
+  if (o.kind == YART_PRIM_SPHERE) {  // sphere.rs:95-110
+    if (STATS) st.v[ST_LIGHT]++;
+    if (!sphere_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
+    const double radius = o.p[3];
+    const double cos_theta_max = sqrt(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
+    const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
+    return 1.0 / solid_angle;
+  }
+  return 0.0;
+}
+__device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g) {
+  if (o.n_xf == 0 && o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:164-171
+    const double x = gen_range(g, o.p[0], o.p[1]);
+    const double z = gen_range(g, o.p[2], o.p[3]);
+    return sub(mk(x, o.p[4], z), origin);
+  }
+  if (o.n_xf == 0 && o.kind == YART_PRIM_SPHERE) {  // sphere.rs:112-118, 11-21
+    const V3 direction = sub(ld3(o.p), origin);
+    const double d2 = len2(direction);
+    const Onb uvw = onb_from_w(direction);
+    const double r1 = gen_f64(g), r2 = gen_f64(g);
+    const double radius = o.p[3];
+    const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / d2) - 1.0);
+    double s, c;
+    sincos_det(2.0 * kPi * r1, s, c);
+    const V3 rs = mk(c * sqrt(1.0 - z * z), s * sqrt(1.0 - z * z), z);
+    return local(uvw, rs);
+  }
+  return mk(1.0, 0.0, 0.0);
+}
+
+// ---------------------------------------------------------------------- materials
+__device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, double wl, V3 p) {
+  const DevTexture& t = S.textures[ti];
+  const int bin = spectrum_bin(wl);
+  if (t.kind == YART_TEX_CHECKER) {  // texture.rs:58-67
+    const double sines = sin_det(10.0 * p.x) * sin_det(10.0 * p.y) * sin_det(10.0 * p.z);
+    return sines < 0.0 ? t.spec[bin] : t.spec_even[bin];
+  }
+  return t.spec[bin];
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, smul(2.0 * dot(v, n), n)); }  // material.rs:75-77
+
+// --------------------------------------------------------------------------- sampling
+__device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double t, double wl, Rng& g) {  // camera.rs:82-94
+  V3 p;
+  for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_disk camera.rs:25-33
+    const double x = gen_range(g, -1.0, 1.0);
+    const double y = gen_range(g, -1.0, 1.0);
+    p = mk(x, y, 0.0);
+    if (!(len2(p) >= 1.0)) break;
+  }
+  const V3 rd = smul(c.lens_radius, p);
+  const V3 offset = add(muls(ld3(c.u), rd.x), muls(ld3(c.v), rd.y));
+  const V3 org = ld3(c.origin);
+  Ray r;
+  r.o = add(org, offset);
+  r.d = sub(sub(add(add(ld3(c.lower_left_corner), smul(s, ld3(c.horizontal))), smul(t, ld3(c.vertical))), org), offset);
+  r.time = gen_range(g, c.time0, c.time1);
+  r.wl = wl;
+  return r;
+}
+
+__device__ __forceinline__ bool covered(uint32_t x, uint32_t w) {  // main.rs:636-647 crop grid
+  const uint32_t cw = w / 8;
+#pragma unroll
+  for (uint32_t col = 0; col < 8; ++col) {
+    const uint32_t x0 = (uint32_t)(((uint64_t)w * col) / 8);
+    if (x >= x0 && x < x0 + cw) return true;
+  }
+  return false;
+}
+
+// Blocks b and b+8 are dealt to one XCD (MI355X_MICROARCH.md §Workgroup dispatch): give each XCD
+// a contiguous run of pixel blocks so neighbouring tiles share that XCD's L2 (speed only).
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  const uint32_t q = n / 8, r = n % 8, xcd = b % 8, k = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+template <bool HAS_MESH, bool STATS>
+__global__ __launch_bounds__(256) void k_render(DevScene S, RenderArgs A) {
+  __shared__ uint32_t s_stack[HAS_MESH ? 4 * kStackSlots * 64 : 1];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t local_blk = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  if (local_blk >= A.n_blocks) return;
+  const uint32_t b = A.shard_index + local_blk * A.shard_count;
+  const uint32_t x = (b % A.blocks_x) * 8 + (lane & 7u), y = (b / A.blocks_x) * 8 + (lane >> 3);
+  const uint32_t W = A.width, H = A.height;
+  const bool active = x < W && y < H && covered(x, W) && covered(y, H);
+  uint32_t* stk = &s_stack[HAS_MESH ? (wave * kStackSlots * 64 + lane) : 0];
+  Stats st;
+  if (STATS) for (int i = 0; i < 8; ++i) st.v[i] = 0;
+
+  const uint32_t pixel = y * W + x;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  uint32_t smp = 0;
+  bool alive = active && A.spp > 0;
+  Rng g;
+  Ray ray;
+  double T = 1.0;
+  uint32_t depth = 0;
+  bool fresh = alive;  // start a sample at the top of the loop
+
+  while (alive) {
+    if (fresh) {  // main.rs:692-698
+      rng_init(g, A.seed, pixel, smp, 0);
+      const double tx = (double)x + gen_f64(g);
+      const double u = tx / (double)(W - 1);
+      const double ty = (double)y + gen_f64(g);
+      const double v = 1.0 - ty / (double)(H - 1);
+      const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
+      ray = camera_ray(A.cam, u, v, wl, g);
+      T = 1.0;
+      depth = A.max_depth;
+      fresh = false;
+    }
+    double R = 0.0;
+    bool term = false;
+    if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
+      R = T * 1.0;
+      term = true;
+    } else {
+      Hit h;
+      int32_t which;
+      if (STATS) st.v[ST_SEGMENTS]++;
+      if (!world_hit<HAS_MESH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
+        const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
+        R = T * S.background[bin];
+        term = true;
+      } else {
+        const DevMaterial& m = S.materials[h.mat];
+        const uint32_t kind = m.kind;
+        if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+          const double att = texture_value(S, m.texture, ray.wl, h.p);
+          const Onb uvw = onb_from_w(h.n);
+          V3 dir;
+          double pdf_val;
+          if (S.n_lights == 0) {
+            (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
+            dir = local(uvw, random_cosine_direction(g));
+            pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
+          } else {
+            if (gen_range(g, 0.0, 1.0) < 0.5) {
+              // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+              const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+              dir = light_random(S.lights[k], h.p, g);
+            } else {
+              dir = local(uvw, random_cosine_direction(g));
+            }
+            const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+            double sum = -0.0;
+            for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], h.p, dir, ray.wl, st);
+            pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
+          }
+          if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+            R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+            term = true;
+          } else {
+            const double cosine = dot(h.n, unit(dir));  // Lambertian::scatter_pdf
+            const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+            T = ((T * att) * spdf) / pdf_val;
+            ray.o = h.p;
+            ray.d = dir;
+            depth--;
+          }
+        } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+          const V3 reflected = reflect(unit(ray.d), h.n);
+          V3 p;
+          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+            p = mk(px, py, pz);
+            if (!(len2(p) >= 1.0)) break;
+          }
+          const double att = texture_value(S, m.texture, ray.wl, h.p);
+          T = T * att;
+          ray.o = h.p;
+          ray.d = add(reflected, smul(m.fuzz, p));
+          depth--;
+        } else if (kind == YART_MAT_DIELECTRIC) {  // material.rs:213-301
+          const double wl2 = ray.wl * ray.wl;
+          const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+          const double n = sqrt(n2);
+          V3 outward;
+          double ni_over_nt, cosine;
+          if (dot(ray.d, h.n) > 0.0) {
+            outward = neg(h.n); ni_over_nt = n; cosine = n * dot(ray.d, h.n) / len(ray.d);
+          } else {
+            outward = h.n; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, h.n) / len(ray.d);
+          }
+          const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
+          const double dt = dot(uv, outward);
+          const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+          V3 out;
+          if (disc > 0.0) {
+            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
+            double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+            r0 = r0 * r0;
+            const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+            out = gen_f64(g) < sch ? reflect(ray.d, h.n) : refracted;
+          } else {
+            out = reflect(ray.d, h.n);
+          }
+          T = T * 1.0;
+          ray.o = h.p;
+          ray.d = out;
+          depth--;
+        } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
+          double emitted = 0.0;
+          if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value(S, m.texture, ray.wl, h.p);
+          R = T * emitted;
+          term = true;
+        }
+      }
+    }
+    if (term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
+      double cx, cy, cz;
+      cie_xyz(ray.wl, cx, cy, cz);
+      double sx = cx * R, sy = cy * R, sz = cz * R;
+      if (!isfinite(sx) || !isfinite(sy) || !isfinite(sz)) {
+        sx = sy = sz = 0.0;
+      } else if (!(sy <= 0.0 || sy <= kMaxLum)) {
+        const double k = kMaxLum / sy;
+        sx = sx * k; sy = sy * k; sz = sz * k;
+      }
+      acc0 = acc0 + sx; acc1 = acc1 + sy; acc2 = acc2 + sz;
+      if (STATS) st.v[ST_SAMPLES]++;
+      smp++;
+      if (smp < A.spp) fresh = true;
+      else alive = false;
+    }
+  }
+  if (active) {
+    double* o = A.out + 3 * (size_t)pixel;
+    o[0] = acc0; o[1] = acc1; o[2] = acc2;
+  }
+  if (STATS) {
+    for (int i = 0; i < 8; ++i)
+      if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
+  }
+}
+
+// ------------------------------------------------------------------- batched closest hit
+__global__ __launch_bounds__(256) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
+                                                   double* __restrict__ hits, int32_t* __restrict__ obj) {
+  __shared__ uint32_t s_stack[4 * kStackSlots * 64];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if (i >= n) return;
+  const double* q = rays + 8 * (size_t)i;
+  Ray r{mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), 0.0, 0.0};
+  Hit h;
+  int32_t which = -1;
+  Stats st;
+  double* o = hits + 8 * (size_t)i;
+  if (world_hit<true, false>(S, r, q[6], q[7], h, which, &s_stack[wave * kStackSlots * 64 + lane], st)) {
+    o[0] = h.t; o[1] = h.p.x; o[2] = h.p.y; o[3] = h.p.z;
+    o[4] = h.n.x; o[5] = h.n.y; o[6] = h.n.z; o[7] = h.ff ? 1.0 : 0.0;
+  } else {
+    for (int k = 0; k < 8; ++k) o[k] = NAN;
+  }
+  obj[i] = which;
+}
+
+// ------------------------------------------------------------------------ finalize
+__device__ __forceinline__ double gamma_channel(double linear) {  // color.rs:93-101
+  linear = fmax(linear, 0.0);
+  if (linear <= 0.0031308) return 12.92 * linear;
+  return 1.055 * pow(linear, 1.0 / 2.4) - 0.055;
+}
+__device__ __forceinline__ uint8_t display_channel(double c) {  // main.rs:461-463
+  if (c != c) return 0;
+  c = c < 0.0 ? 0.0 : (c > 0.999 ? 0.999 : c);
+  const double m = 256.0 * c;
+  return m >= 255.0 ? (uint8_t)255 : (uint8_t)(int)m;
+}
+__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ xyz, uint32_t w, uint32_t h, uint32_t spp,
+                                                  uint8_t* __restrict__ rgba) {  // main.rs:710-718
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w * h) return;
+  const uint32_t x = i % w, y = i / w;
+  uchar4 out = make_uchar4(0, 0, 0, 0);
+  if (covered(x, w) && covered(y, h)) {
+    V3 v = mk(xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1], xyz[3 * (size_t)i + 2]);
+    v = divs(muls(v, kMaxLambda - kMinLambda), kCieYIntegral * (double)spp);
+    const double r = 2.6896552 * v.x - 1.2758621 * v.y - 0.4137931 * v.z;  // XYZ::into_rgb color.rs:209-213
+    const double gg = -1.0221082 * v.x + 1.9782866 * v.y + 0.0438216 * v.z;
+    const double b = 0.0612245 * v.x - 0.2244898 * v.y + 1.1632653 * v.z;
+    out = make_uchar4(display_channel(gamma_channel(r)), display_channel(gamma_channel(gg)),
+                      display_channel(gamma_channel(b)), 255);
+  }
+  reinterpret_cast<uchar4*>(rgba)[i] = out;
+}
+
+// --------------------------------------------------------------------------- probes
+__global__ void k_probe_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, double* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  Rng g;
+  rng_init(g, seed, pixel, sample, 0);
+  for (uint32_t i = 0; i < n; ++i) out[i] = gen_f64(g);
+}
+__global__ void k_probe_math(int op, const double* a, const double* b, uint32_t n, double* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s, c;
+  switch (op) {
+    case 0: out[i] = sqrt(a[i]); break;
+    case 1: out[i] = a[i] / b[i]; break;
+    case 2: sincos_det(a[i], s, c); out[i] = s; break;
+    case 3: sincos_det(a[i], s, c); out[i] = c; break;
+    default: out[i] = pow(a[i], b[i]); break;
+  }
+}
+
+// ------------------------------------------------------------------------- launchers
+hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream) {
+  const uint32_t grid = (a.n_blocks + 3) / 4;
+  if (grid == 0) return hipSuccess;
+  if (s.has_mesh) {
+    if (stats) hipLaunchKernelGGL((k_render<true, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+  } else {
+    if (stats) hipLaunchKernelGGL((k_render<false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,
+                            hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
+  return hipGetLastError();
+}
+hipError_t launch_finalize(const double* xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba, hipStream_t stream) {
+  const uint32_t n = w * h;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, stream, xyz, w, h, spp, rgba);
+  return hipGetLastError();
+}
+hipError_t launch_probe_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_probe_rng, dim3(1), dim3(64), 0, stream, seed, pixel, sample, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_probe_math(int op, const double* a, const double* b, uint32_t n, double* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_math, dim3((n + 255) / 256), dim3(256), 0, stream, op, a, b, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace yart_dev
