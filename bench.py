@@ -31,6 +31,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
 import yart  # noqa: E402
+from yart.shard import assemble_frame  # noqa: E402
 
 WORKLOAD = dict(scene="cornell-box", width=800, height=800, spp=256, max_depth=50)
 
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-spp", type=int, default=128, help="spp of the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
     ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
     return ap.parse_args()
@@ -114,8 +115,7 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         if world > 1:
-            frame.copy_(mine)
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+            assemble_frame(mine, frame, dist, dst=0)
         if rank == 0:
             rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
                                              yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(stream.cuda_stream))

@@ -1,0 +1,75 @@
+"""The C ABI libraries load and export every symbol their headers declare (no GPU calls), and the
+ctypes mirror used by tests/bench matches the C layout."""
+import ctypes as C
+import re
+import subprocess
+
+import pytest
+
+import yart
+from yart import abi
+
+
+def declared(header):
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(yart_[a-z0-9_]+)\s*\(", text)) - {"yart_progress_fn"})
+
+
+def exported(so):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(so)], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_device_library_exports_every_declared_symbol(repo):
+    so = repo / "yet-another-raytracer_amd" / "lib" / "libyart.so"
+    names = declared(repo / "include" / "yart.h")
+    assert set(names) == set(abi.DEVICE_SYMBOLS)
+    missing = set(names) - exported(so)
+    assert not missing, missing
+
+
+def test_host_library_exports_every_declared_symbol(repo):
+    so = repo / "yet-another-raytracer_amd" / "lib" / "libyart_host.so"
+    names = declared(repo / "include" / "yart_host.h")
+    assert set(names) == set(abi.HOST_SYMBOLS)
+    missing = set(names) - exported(so)
+    assert not missing, missing
+
+
+def test_device_library_loads_without_gpu():
+    L = yart.load_device()  # loading must not touch the GPU
+    assert L.yart_version().decode().startswith("yart-mi355x")
+    assert L.yart_last_error().decode() == ""
+
+
+def test_device_library_has_gfx950_code_object(repo):
+    so = repo / "yet-another-raytracer_amd" / "lib" / "libyart.so"
+    data = so.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle entry of the embedded code object
+    assert b"k_render" in data
+
+
+def test_struct_layouts_match_c(repo, tmp_path):
+    src = tmp_path / "sizes.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "yart.h"
+#include "yart_host.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(yart_texture), sizeof(yart_material),
+         sizeof(yart_xform), sizeof(yart_object), sizeof(yart_mesh), sizeof(yart_scene_desc), sizeof(yart_camera),
+         sizeof(yart_render_params), sizeof(yart_scene_info), sizeof(yart_render_stats), sizeof(yart_render_defaults),
+         sizeof(yart_cli), sizeof(yart_render_options));
+  printf("%zu %zu %zu\n", offsetof(yart_object, p), offsetof(yart_scene_desc, background), offsetof(yart_cli, seed));
+  return 0;
+}
+''')
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-I", str(repo / "include"), str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    want = [abi.Texture, abi.Material, abi.Xform, abi.Object, abi.Mesh, abi.SceneDesc, abi.Camera, abi.RenderParams,
+            abi.SceneInfo, abi.RenderStats, abi.RenderDefaults, abi.Cli, abi.RenderOptions]
+    assert [int(x) for x in got[0].split()] == [C.sizeof(t) for t in want]
+    assert [int(x) for x in got[1].split()] == [abi.Object.p.offset, abi.SceneDesc.background.offset, abi.Cli.seed.offset]

@@ -1,0 +1,28 @@
+#!/bin/bash
+# rocprofv3 passes over bench.py (one gpurun call). Pass 1: kernel trace + stats. Passes 2-3:
+# PMC counters, one block of counters per pass (FETCH_SIZE and WRITE_SIZE cannot share a pass
+# on gfx950), each with --kernel-trace only. Outputs under gpurun_out/prof_*; summaries are then
+# copied into profiles/ by hand.
+set -u
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH_ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --cpu-spp 0 --no-stats"}
+step() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 5 "$OUT/$name.log"
+  case $rc in 0) return 0;; *) echo "stopping after rc=$rc"; exit $rc;; esac
+}
+PASSES=${PASSES:-"list trace fetch write valu"}
+for p in $PASSES; do
+  case $p in
+    list)  step prof_list 120 rocprofv3 -L ;;
+    trace) step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o run -- python3 "$REPO/bench.py" $BENCH_ARGS ;;
+    fetch) step prof_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -o run -- python3 "$REPO/bench.py" $BENCH_ARGS ;;
+    write) step prof_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/prof_write" -o run -- python3 "$REPO/bench.py" $BENCH_ARGS ;;
+    valu)  step prof_valu 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/prof_valu" -o run -- python3 "$REPO/bench.py" $BENCH_ARGS ;;
+  esac
+done

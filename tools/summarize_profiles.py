@@ -1,0 +1,65 @@
+"""Summarize a tools/profile.sh run (gpurun_out/prof_*) into profiles/ (committed evidence).
+
+    python tools/summarize_profiles.py <round-tag> [kernel-substring]
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats of the bench command),
+profiles/<tag>_pmc.json (per-launch PMC values of the render kernel, HBM bytes with the gfx950
+correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) x 1024 x 2 + WRITE_SIZE (KiB) x 1024)
+and profiles/pmc_render_cornell.json (what bench.py reads for roofline.traffic).
+"""
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+OUT = ROOT / "gpurun_out"
+PROF = ROOT / "profiles"
+
+
+def per_launch(pass_dir, kernel):
+    rows = list(csv.DictReader(open(OUT / pass_dir / "run_counter_collection.csv")))
+    vals = {}
+    for r in rows:
+        if kernel in r["Kernel_Name"]:
+            vals.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
+            vals[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in vals.items()}, rows
+
+
+def main():
+    tag = sys.argv[1]
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<false, false>"
+    PROF.mkdir(exist_ok=True)
+    shutil.copy(OUT / "prof_trace" / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
+    summary = {"kernel": kernel, "source": "tools/profile.sh (rocprofv3 --pmc, one counter block per pass)"}
+    for p in ("prof_fetch", "prof_write", "prof_valu"):
+        if (OUT / p / "run_counter_collection.csv").exists():
+            v, rows = per_launch(p, kernel)
+            summary.update(v)
+            for r in rows:
+                if kernel in r["Kernel_Name"]:
+                    summary.setdefault("vgpr", int(r["VGPR_Count"]))
+                    summary.setdefault("sgpr", int(r["SGPR_Count"]))
+                    summary.setdefault("lds_bytes", int(r["LDS_Block_Size"]))
+                    summary.setdefault("grid", int(r["Grid_Size"]))
+                    break
+    stats = list(csv.DictReader(open(PROF / f"{tag}_kernel_stats.csv")))
+    for s in stats:
+        if kernel in s["Name"]:
+            summary["avg_duration_ns"] = float(s["AverageNs"])
+            summary["calls"] = int(s["Calls"])
+    fetch = summary.get("FETCH_SIZE")
+    write = summary.get("WRITE_SIZE")
+    if fetch is not None and write is not None:
+        summary["hbm_bytes_per_launch"] = int(fetch * 1024 * 2 + write * 1024)
+        summary["hbm_bytes_note"] = "FETCH_SIZE x2 (gfx950 reports half of wide reads) + WRITE_SIZE, KiB -> B"
+    (PROF / f"{tag}_pmc.json").write_text(json.dumps(summary, indent=1) + "\n")
+    if "cornell" in tag or tag.endswith("_render"):
+        (PROF / "pmc_render_cornell.json").write_text(json.dumps(summary, indent=1) + "\n")
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

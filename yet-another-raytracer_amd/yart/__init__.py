@@ -158,9 +158,15 @@ class DeviceScene:
     """A scene resident in one GPU's HBM (yart_scene_create)."""
 
     def __init__(self, desc, device=0):
+        """desc: a POINTER(SceneDesc), or an object owning one (Preset) - kept alive until create
+        returns, since yart_scene_create copies everything it needs."""
         L = load_device()
+        owner = desc
+        if hasattr(desc, "desc"):
+            desc = desc.desc
         self._s = C.c_void_p()
         _check_dev(L.yart_scene_create(device, desc, C.byref(self._s)))
+        del owner
         self.device = device
 
     def close(self):
