@@ -44,3 +44,9 @@ clean:
 	rm -rf $(LIB) $(BIN) $(GEN)
 	$(MAKE) -C $(ROOT)/oracle clean
 .PHONY: all host device cli oracle clean
+
+# A/B builds for tools/ab.py: make variant NAME=x DEFS="-DYART_FOO"
+variant: $(GEN)/cie_xyz.inc $(GEN)/smits.inc
+	@mkdir -p $(LIB)/variants
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIB)/variants/libyart_$(NAME).so $(DEV_SRCS)
+.PHONY: variant

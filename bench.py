@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-spp", type=int, default=128, help="spp of the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
     ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
+    ap.add_argument("--spu", type=int, default=0, help="samples per work unit (0 = library's choice)")
     return ap.parse_args()
 
 
@@ -96,7 +97,7 @@ def main():
 
     preset = yart.Preset(WORKLOAD["scene"])
     cam = preset.camera(W, H)
-    prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world)
+    prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world, samples_per_unit=a.spu)
     scene = yart.DeviceScene(preset.desc, device=local)
     mine = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)   # this rank's blocks, zeros elsewhere
     frame = torch.zeros_like(mine) if world > 1 else mine

@@ -157,6 +157,12 @@ typedef struct yart_render_params {
                          is unseedable, see DESIGN.md "RNG" */
   uint32_t shard_index;
   uint32_t shard_count; /* 0 or 1 = whole frame */
+  /* Samples one wave renders per 8x8 block before handing over (0 = chosen by the library from
+   * the device size). Below spp, each sample's value goes to an HBM scratch and a second kernel
+   * adds them per pixel in sample order, so the sums are bitwise those of one sequential loop
+   * (main.rs:691-708) whatever the split; it only changes how finely work spreads over CUs. */
+  uint32_t samples_per_unit;
+  uint32_t reserved;
 } yart_render_params;
 
 typedef struct yart_scene yart_scene; /* opaque, device resident */

@@ -140,6 +140,43 @@ def test_render_bitwise_equal_to_oracle(dev, scene, W, H, spp, depth):
     assert (gpu[cov].sum(axis=-1) != 0).mean() > 0.05
 
 
+@pytest.mark.parametrize("scene,spu", [("cornell-box", 1), ("cornell-box", 3), ("cornell-box", 7), ("david", 2),
+                                       ("random-scene", 5)])
+def test_chunked_samples_bitwise_equal_to_sequential_sum(dev, scene, spu):
+    """samples_per_unit < spp: per-sample values go through HBM and k_accumulate adds them in
+    sample order; the sums must not change (main.rs:707's sequential +=)."""
+    p = yart.Preset(scene)
+    W, H, spp = 40, 24, 8
+    cam = p.camera(W, H)
+    s = yart.DeviceScene(p)
+    fused = s.render(cam, yart.render_params(W, H, spp, 50, samples_per_unit=spp))  # one unit per block
+    chunked = s.render(cam, yart.render_params(W, H, spp, 50, samples_per_unit=spu))
+    np.testing.assert_array_equal(chunked, fused)
+    np.testing.assert_array_equal(chunked, O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
+
+
+def test_chunked_multi_pass_and_shards(dev, monkeypatch):
+    """A scratch budget of a few samples forces several accumulate passes; with shards too."""
+    p = yart.Preset("cornell-box")
+    W, H, spp = 48, 40, 10
+    cam = p.camera(W, H)
+    s = yart.DeviceScene(p)
+    ref = O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50))
+    monkeypatch.setenv("YART_SCRATCH_BYTES", str(3 * 48 * 64 * 24))  # 3 samples x (48/8*40/8 blocks)
+    parts = [s.render(cam, yart.render_params(W, H, spp, 50, shard_index=i, shard_count=2, samples_per_unit=1))
+             for i in range(2)]
+    np.testing.assert_array_equal(parts[0] + parts[1], ref)
+
+
+def test_auto_chunking_at_full_device_scale(dev):
+    """A small frame on a 256-CU device is auto-split into sample chunks; still bitwise."""
+    p = yart.Preset("cornell-box")
+    W, H, spp = 64, 64, 64
+    cam = p.camera(W, H)
+    g = yart.DeviceScene(p).render(cam, yart.render_params(W, H, spp, 50))
+    np.testing.assert_array_equal(g, O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
+
+
 def test_shards_partition_the_frame(dev):
     p = yart.Preset("cornell-box")
     W, H, spp = 72, 48, 4

@@ -1,0 +1,91 @@
+"""Time every BASELINE.json config on one MI355X (bench.py covers only the headline C2).
+
+    python tools/bench_configs.py [--configs C2,C3,C4,C5] [--spp-scale 1.0] [--cpu]
+
+One untimed warm-up launch at 1 spp, then one timed frame (HIP events on the launch stream),
+then an instrumented launch (work counters) of the same frame. Prints one JSON line per config.
+C5 (david 1920x1080x1024, quoted on 8 GPUs) is timed here on one GPU and as one shard of 8."""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
+sys.path.insert(0, str(ROOT / "tests"))
+import yart  # noqa: E402
+
+CONFIGS = {
+    "C1": ("two-spheres", 400, 225, 16, 8),
+    "C2": ("cornell-box", 800, 800, 256, 50),
+    "C3": ("random-scene", 1200, 800, 500, 50),
+    "C4": ("bunny", 800, 800, 512, 50),
+    "C5": ("david", 1920, 1080, 1024, 50),
+}
+
+
+def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False):
+    p = yart.Preset(scene_name)
+    cam = p.camera(w, h)
+    s = yart.DeviceScene(p)
+    out = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
+    st = torch.cuda.current_stream()
+    s.render_async(cam, yart.render_params(w, h, 1, depth, shard_index=shard[0], shard_count=shard[1]),
+                   out.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    prm = yart.render_params(w, h, spp, depth, shard_index=shard[0], shard_count=shard[1])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    s.render_async(cam, prm, out.data_ptr(), st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1)
+    n = w * h * spp // shard[1]
+    line = {"config": name, "scene": scene_name, "stand_in": p.stand_in or None, "size": f"{w}x{h}x{spp}",
+            "depth": depth, "shard": f"{shard[0]}/{shard[1]}", "kernel_ms": round(ms, 2), "wall_s": round(wall, 3),
+            "Msamples_per_s": round(n / (ms * 1e-3) / 1e6, 2)}
+    if stats:
+        _, c = s.render_with_stats(cam, prm)
+        line["counts"] = {"samples": c.samples, "segments": c.segments, "prim_tests": c.prim_tests,
+                          "node_visits": c.node_visits, "leaf_visits": c.leaf_visits, "leaf_tris": c.leaf_tris,
+                          "light_tests": c.light_tests}
+        info = s.info()
+        if info.bvh_nodes:
+            # algorithmic bytes of the traversal: 128 B per inner node visit,
+            # 144 B per leaf block, 72 B of normals per accepted hit ~ segment
+            b = 128 * c.node_visits + 144 * c.leaf_visits + 72 * c.segments
+            line["traversal_bytes"] = b
+            line["traversal_GBps"] = round(b / (ms * 1e-3) / 1e9, 1)
+    if cpu:
+        import oracle_lib as O
+        cspp = max(1, spp // 64)
+        t0 = time.perf_counter()
+        O.OracleScene(p.desc).render(cam, yart.render_params(w, h, cspp, depth), threads=16)
+        dt = time.perf_counter() - t0
+        line["cpu_Msamples_per_s_16thr"] = round(w * h * cspp / dt / 1e6, 3)
+        line["cpu_sample"] = f"{w}x{h}x{cspp}"
+    print(json.dumps(line), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C1,C2,C3,C4,C5")
+    ap.add_argument("--spp-scale", type=float, default=1.0)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--no-stats", action="store_true")
+    a = ap.parse_args()
+    for c in a.configs.split(","):
+        scene, w, h, spp, depth = CONFIGS[c]
+        spp = max(1, int(spp * a.spp_scale))
+        if c == "C5":
+            run(c + "-shard", scene, w, h, spp, depth, shard=(0, 8), stats=not a.no_stats, cpu=False)
+        run(c, scene, w, h, spp, depth, stats=not a.no_stats, cpu=a.cpu)
+
+
+if __name__ == "__main__":
+    main()

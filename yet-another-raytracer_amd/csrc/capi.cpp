@@ -4,7 +4,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -108,12 +111,17 @@ DevObject to_dev(const yart_object& o) {
 
 struct yart_scene {
   int device = 0;
+  int cu_count = 256;
   DevScene dev{};
   std::vector<void*> owned;
   yart_scene_info info{};
+  // Per-stream scratch for the chunked render path (grown on demand, reused across frames).
+  std::mutex scratch_mu;
+  std::map<hipStream_t, std::pair<double*, size_t>> scratch;
   ~yart_scene() {
     DeviceGuard g(device);
     for (void* p : owned) (void)hipFree(p);
+    for (auto& kv : scratch) (void)hipFree(kv.second.first);
   }
 };
 
@@ -194,6 +202,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   auto s = std::make_unique<yart_scene>();
   s->device = device;
   DeviceGuard guard(device);
+  if (hipDeviceGetAttribute(&s->cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || s->cu_count <= 0)
+    s->cu_count = 256;
   uint64_t bytes = 0;
   DevScene& ds = s->dev;
   HIP_TRY(upload(s->owned, objs.data(), objs.size(), &ds.objects, bytes), "upload objects");
@@ -247,8 +257,75 @@ static int make_args(const yart_scene* s, const yart_camera* cam, const yart_ren
   a.blocks_x = (p->width + 7) / 8;
   const uint32_t total = a.blocks_x * ((p->height + 7) / 8);
   a.n_blocks = total > p->shard_index ? (total - p->shard_index + sc - 1) / sc : 0;
+  a.s_begin = 0; a.s_count = p->spp; a.chunk = p->spp ? p->spp : 1; a.n_chunks = 1;
   a.out = out;
+  a.scratch = nullptr;
   a.stats = nullptr;
+  return YART_OK;
+}
+
+// Work decomposition. A unit is one wave rendering one 8x8 block for `chunk` consecutive samples.
+// With chunk = spp (one unit per block) the kernel keeps the per-pixel sums in registers (fused).
+// When the shard has too few blocks to fill the device several times over (strong scaling, small
+// frames) the samples are split into chunks; each sample's value then goes to HBM and
+// k_accumulate adds them per pixel in sample order, so the sums do not depend on the split.
+struct Plan { uint32_t chunk, pass_spp; };
+static Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
+  const uint32_t spp = a.spp;
+  if (spp == 0 || a.n_blocks == 0) return {spp ? spp : 1, spp};
+  uint32_t chunk;
+  if (requested) {
+    chunk = requested < spp ? requested : spp;
+  } else {
+    // aim for ~8 rounds of resident waves (4 per SIMD x 4 SIMDs per CU)
+    const uint64_t target = 8ull * (uint64_t)s->cu_count * 16ull;
+    uint64_t chunks = (target + a.n_blocks - 1) / a.n_blocks;
+    if (chunks <= 1) return {spp, spp};
+    if (chunks > spp) chunks = spp;
+    chunk = (uint32_t)((spp + chunks - 1) / chunks);
+  }
+  if (chunk >= spp) return {spp, spp};
+  const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
+  uint64_t budget = 4ull << 30;
+  if (const char* e = std::getenv("YART_SCRATCH_BYTES")) budget = std::strtoull(e, nullptr, 0);
+  uint64_t pass = budget / per_sample;
+  pass = pass / chunk * chunk;
+  if (pass < chunk) pass = chunk;
+  if (pass > spp) pass = spp;
+  return {chunk, (uint32_t)pass};
+}
+
+static int get_scratch(yart_scene* s, hipStream_t stream, size_t bytes, double** out) {
+  std::lock_guard<std::mutex> lk(s->scratch_mu);
+  auto& e = s->scratch[stream];
+  if (e.second < bytes) {
+    if (e.first) HIP_TRY(hipFree(e.first), "hipFree scratch");
+    e.first = nullptr; e.second = 0;
+    HIP_TRY(hipMalloc(&e.first, bytes), "hipMalloc scratch");
+    e.second = bytes;
+  }
+  *out = e.first;
+  return YART_OK;
+}
+
+static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream) {
+  const Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
+  if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
+    HIP_TRY(launch_render(s->dev, a, stats, stream), "launch k_render");
+    return YART_OK;
+  }
+  double* scratch = nullptr;
+  if (int rc = get_scratch(s, stream, (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double), &scratch)) return rc;
+  for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp) {
+    RenderArgs b = a;
+    b.s_begin = s0;
+    b.s_count = a.spp - s0 < pl.pass_spp ? a.spp - s0 : pl.pass_spp;
+    b.chunk = pl.chunk;
+    b.n_chunks = (b.s_count + pl.chunk - 1) / pl.chunk;
+    b.scratch = scratch;
+    HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
+    HIP_TRY(launch_accumulate(b, s0 == 0, stream), "launch k_accumulate");
+  }
   return YART_OK;
 }
 
@@ -258,7 +335,7 @@ int yart_render_async(yart_scene* s, const yart_camera* cam, const yart_render_p
   if (int rc = make_args(s, cam, p, d_xyz_sum, a)) return rc;
   if (!d_xyz_sum) return fail(YART_ERR_INVALID, "null output");
   DeviceGuard g(s->device);
-  HIP_TRY(launch_render(s->dev, a, false, (hipStream_t)stream), "launch k_render");
+  if (int rc = launch_frame(s, a, p->samples_per_unit, false, (hipStream_t)stream)) return rc;
   return ok();
 }
 
@@ -281,7 +358,7 @@ static int render_host(yart_scene* s, const yart_camera* cam, const yart_render_
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
   a.stats = d_stats;
-  HIP_TRY(launch_render(s->dev, a, stats != nullptr, nullptr), "launch k_render");
+  if (int rc = launch_frame(s, a, p->samples_per_unit, stats != nullptr, nullptr)) return rc;
   HIP_TRY(hipDeviceSynchronize(), "k_render");
   HIP_TRY(hipMemcpy(host_out, d_out, bytes, hipMemcpyDeviceToHost), "copy output");
   if (stats) {

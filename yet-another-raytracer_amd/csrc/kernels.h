@@ -15,11 +15,17 @@ struct RenderArgs {
   uint32_t shard_index, shard_count;
   uint32_t blocks_x;  // ceil(width / 8)
   uint32_t n_blocks;  // 8x8-pixel blocks owned by this shard
-  double* out;        // width * height * 3
+  // Work units = n_blocks x n_chunks; unit u renders block u % n_blocks for samples
+  // [s_begin + (u / n_blocks) * chunk, ... + chunk) clipped to [s_begin, s_begin + s_count).
+  uint32_t s_begin, s_count, chunk, n_chunks;
+  double* out;        // width * height * 3 (fused path: final sums; written by k_accumulate otherwise)
+  double* scratch;    // null = fused; else n_blocks * s_count * 64 * 3 per-sample XYZ
   unsigned long long* stats;  // 8 counters (STATS build only)
 };
 
 hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream);
+// Adds a pass's per-sample values onto the per-pixel sums in sample order (first pass from 0).
+hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t stream);
 hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,
                             hipStream_t stream);
 hipError_t launch_finalize(const double* xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba, hipStream_t stream);

@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
       rcs[g] = yart_scene_create(g, yart_preset_desc(preset), &s);
       if (rcs[g] == YART_OK) {
         yart_render_params p{o.width, o.height, (uint32_t)o.samples_per_pixel, (uint32_t)o.max_depth, 0x59415254ull,
-                             (uint32_t)g, (uint32_t)gpus};
+                             (uint32_t)g, (uint32_t)gpus, 0, 0};
         if (cli.seed) p.seed = cli.seed;
         rcs[g] = yart_render(s, &cam, &p, parts[g].data(), nullptr, nullptr);
       }

@@ -70,7 +70,7 @@ def load_device():
     global _dev
     if _dev is not None:
         return _dev
-    path = LIB_DIR / "libyart.so"
+    path = Path(os.environ.get("YART_DEVICE_LIB", LIB_DIR / "libyart.so"))  # A/B builds (tools/ab.py)
     if not path.exists():
         raise FileNotFoundError(f"{path} is not built; the HIP path has no fallback")
     L = C.CDLL(str(path))
@@ -150,8 +150,8 @@ def make_camera(lookfrom, lookat, vfov, aspect, aperture, focus_dist=10.0, vup=(
     return cam
 
 
-def render_params(width, height, spp, max_depth, seed=DEFAULT_SEED, shard_index=0, shard_count=1):
-    return abi.RenderParams(width, height, spp, max_depth, seed, shard_index, shard_count)
+def render_params(width, height, spp, max_depth, seed=DEFAULT_SEED, shard_index=0, shard_count=1, samples_per_unit=0):
+    return abi.RenderParams(width, height, spp, max_depth, seed, shard_index, shard_count, samples_per_unit, 0)
 
 
 class DeviceScene:

@@ -52,7 +52,8 @@ class Camera(C.Structure):
 
 class RenderParams(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32),
-                ("seed", C.c_uint64), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
+                ("seed", C.c_uint64), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
+                ("samples_per_unit", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class SceneInfo(C.Structure):
