@@ -275,16 +275,17 @@ static Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
   if (spp == 0 || a.n_blocks == 0) return {spp ? spp : 1, spp};
   uint32_t chunk;
   if (requested) {
-    chunk = requested < spp ? requested : spp;
+    if (requested >= spp) return {spp, spp};  // explicit one-unit-per-block: the fused kernel
+    chunk = requested;
   } else {
-    // aim for ~8 rounds of resident waves (4 per SIMD x 4 SIMDs per CU)
-    const uint64_t target = 8ull * (uint64_t)s->cu_count * 16ull;
+    // ~16 rounds of resident waves (4 per SIMD x 4 SIMDs per CU) so the expensive blocks (glass,
+    // light) do not leave a tail, in multiples of 8 chunks so the 8 XCDs get equal shares.
+    const uint64_t target = 16ull * (uint64_t)s->cu_count * 16ull;
     uint64_t chunks = (target + a.n_blocks - 1) / a.n_blocks;
-    if (chunks <= 1) return {spp, spp};
+    chunks = (chunks + 7) / 8 * 8;
     if (chunks > spp) chunks = spp;
     chunk = (uint32_t)((spp + chunks - 1) / chunks);
   }
-  if (chunk >= spp) return {spp, spp};
   const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
   uint64_t budget = 4ull << 30;
   if (const char* e = std::getenv("YART_SCRATCH_BYTES")) budget = std::strtoull(e, nullptr, 0);

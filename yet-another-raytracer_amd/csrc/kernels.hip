@@ -532,36 +532,70 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 #ifndef YART_WAVES_PER_EU
 #define YART_WAVES_PER_EU 4  // 128 VGPRs -> 4 waves per SIMD (+5% over 3 on the cornell box)
 #endif
-template <bool HAS_MESH, bool STATS>
+// DYN (chunked path only): the unit's 64 pixels x `chunk` samples form a job list that the wave's
+// lanes pull from dynamically — a lane whose path ends takes the next (pixel, sample) job, the
+// wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
+// no lane idles while another still has samples of its own pixel left. Safe because each
+// (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
+template <bool HAS_MESH, bool STATS, bool DYN>
 __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[HAS_MESH ? 4 * kStackSlots * 64 : 1];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
+  // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
+  // one XCD all the expensive glass-sphere blocks: 1,960 vs 2,507 Msamples/s measured.)
   const uint32_t work = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
   if (work >= A.n_blocks * A.n_chunks) return;
   const uint32_t local_blk = work % A.n_blocks, chunk_id = work / A.n_blocks;
   const uint32_t b = A.shard_index + local_blk * A.shard_count;
-  const uint32_t x = (b % A.blocks_x) * 8 + (lane & 7u), y = (b / A.blocks_x) * 8 + (lane >> 3);
+  const uint32_t bx0 = (b % A.blocks_x) * 8, by0 = (b / A.blocks_x) * 8;
+  uint32_t slot = lane;  // pixel slot in the 8x8 block this lane is working on
+  uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kStackSlots * 64 + lane) : 0];
   Stats st;
   if (STATS) for (int i = 0; i < 8; ++i) st.v[i] = 0;
 
-  const uint32_t pixel = y * W + x;
+  uint32_t pixel = y * W + x;
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   const uint32_t s_end = A.s_begin + A.s_count;
-  uint32_t smp = A.s_begin + chunk_id * A.chunk;
-  const uint32_t s_stop = smp + A.chunk < s_end ? smp + A.chunk : s_end;
-  // scratch row of this lane: [local_blk][sample - s_begin][lane][xyz]
-  double* srow = A.scratch ? A.scratch + 3 * ((size_t)local_blk * A.s_count * 64 + lane) : nullptr;
-  bool alive = active && smp < s_stop;
+  const uint32_t s_lo = A.s_begin + chunk_id * A.chunk;
+  const uint32_t s_stop = s_lo + A.chunk < s_end ? s_lo + A.chunk : s_end;
+  uint32_t smp = s_lo;
+  // scratch of this unit's block: [local_blk][sample - s_begin][slot][xyz]
+  double* const sblk = A.scratch ? A.scratch + 3 * (size_t)local_blk * A.s_count * 64 : nullptr;
+  const uint32_t n_jobs = (s_stop > s_lo ? s_stop - s_lo : 0) * 64;
+  uint32_t next_job = 0;  // wave-uniform (DYN)
+  bool need = true;       // DYN: this lane wants a job
+  bool alive = DYN ? (n_jobs > 0) : (active && smp < s_stop);
   Rng g;
   Ray ray;
   double T = 1.0;
   uint32_t depth = 0;
-  bool fresh = alive;  // start a sample at the top of the loop
+  bool fresh = !DYN && alive;  // start a sample at the top of the loop
 
   while (alive) {
+    if (DYN) {
+      const uint64_t m = __ballot(need);
+      if (need) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t job = next_job + rank;
+        if (job >= n_jobs) {
+          alive = false;
+        } else {
+          slot = job & 63u;
+          smp = s_lo + (job >> 6);
+          x = bx0 + (slot & 7u);
+          y = by0 + (slot >> 3);
+          pixel = y * W + x;
+          if (x < W && y < H && covered(x, W) && covered(y, H)) { fresh = true; need = false; }
+        }
+      }
+      next_job += (uint32_t)__popcll(m);
+      if (!alive) break;
+      if (need) continue;  // the job's pixel is outside the crop grid: take another
+    }
     if (fresh) {  // main.rs:692-698
       rng_init(g, A.seed, pixel, smp, 0);
       const double tx = (double)x + gen_f64(g);
@@ -682,19 +716,20 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
         const double k = kMaxLum / sy;
         sx = sx * k; sy = sy * k; sz = sz * k;
       }
-      if (srow) {  // chunked: k_accumulate adds the samples in order
-        double* q = srow + (size_t)(smp - A.s_begin) * 64 * 3;
+      if (STATS) st.v[ST_SAMPLES]++;
+      if (DYN) {  // chunked: k_accumulate adds the samples in order
+        double* q = sblk + 3 * ((size_t)(smp - A.s_begin) * 64 + slot);
         q[0] = sx; q[1] = sy; q[2] = sz;
+        need = true;
       } else {
         acc0 = acc0 + sx; acc1 = acc1 + sy; acc2 = acc2 + sz;
+        smp++;
+        if (smp < s_stop) fresh = true;
+        else alive = false;
       }
-      if (STATS) st.v[ST_SAMPLES]++;
-      smp++;
-      if (smp < s_stop) fresh = true;
-      else alive = false;
     }
   }
-  if (active && !srow) {
+  if (!DYN && active) {
     double* o = A.out + 3 * (size_t)pixel;
     o[0] = acc0; o[1] = acc1; o[2] = acc2;
   }
@@ -807,12 +842,15 @@ hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t s
 hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream) {
   const uint32_t grid = (a.n_blocks * a.n_chunks + 3) / 4;
   if (grid == 0) return hipSuccess;
+  const bool dyn = a.scratch != nullptr;  // stats launches are always fused (see capi.cpp)
   if (s.has_mesh) {
-    if (stats) hipLaunchKernelGGL((k_render<true, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (stats) hipLaunchKernelGGL((k_render<true, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<true, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
   } else {
-    if (stats) hipLaunchKernelGGL((k_render<false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (stats) hipLaunchKernelGGL((k_render<false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
   }
   return hipGetLastError();
 }
