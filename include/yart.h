@@ -216,6 +216,13 @@ int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lo
 int yart_render_async(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
                       double* d_xyz_sum, void* hip_stream);
 
+/* Device time of the kernels of every frame launched on `hip_stream` since the previous call,
+ * from HIP events recorded on that stream around each launch: summed render-kernel time, summed
+ * in-order accumulate time (0 for frames that ran fused) and the number of frames. Call after the
+ * stream has finished those frames; the events are then recycled. */
+int yart_frame_timing(yart_scene* scene, void* hip_stream, double* render_ms, double* accumulate_ms,
+                      uint32_t* frames);
+
 /* Same, with host output and an optional progress callback (called on this thread). */
 int yart_render(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
                 double* xyz_sum_out, yart_progress_fn progress, void* user);

@@ -30,7 +30,7 @@ def per_launch(pass_dir, kernel):
 
 def main():
     tag = sys.argv[1]
-    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<false, false>"
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<false, false, true>"
     PROF.mkdir(exist_ok=True)
     shutil.copy(OUT / "prof_trace" / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
     summary = {"kernel": kernel, "source": "tools/profile.sh (rocprofv3 --pmc, one counter block per pass)"}

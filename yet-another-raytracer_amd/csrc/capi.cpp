@@ -118,10 +118,17 @@ struct yart_scene {
   // Per-stream scratch for the chunked render path (grown on demand, reused across frames).
   std::mutex scratch_mu;
   std::map<hipStream_t, std::pair<double*, size_t>> scratch;
+  // kernel-boundary events of the frames launched per stream and not yet read
+  std::map<hipStream_t, std::vector<std::vector<hipEvent_t>>> frames;
+  std::vector<hipEvent_t> event_pool;
   ~yart_scene() {
     DeviceGuard g(device);
     for (void* p : owned) (void)hipFree(p);
     for (auto& kv : scratch) (void)hipFree(kv.second.first);
+    for (auto& kv : frames)
+      for (auto& f : kv.second)
+        for (hipEvent_t e : f) (void)hipEventDestroy(e);
+    for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
   }
 };
 
@@ -309,25 +316,93 @@ static int get_scratch(yart_scene* s, hipStream_t stream, size_t bytes, double**
   return YART_OK;
 }
 
+// HIP events around every kernel of each frame launched on a stream, kept until
+// yart_frame_timing reads (and recycles) them.
+static int timing_events(yart_scene* s, hipStream_t stream, size_t n, std::vector<hipEvent_t>** out) {
+  std::lock_guard<std::mutex> lk(s->scratch_mu);
+  auto& frames = s->frames[stream];
+  if (frames.size() >= 4096) {  // never read: recycle the oldest frame's events
+    for (hipEvent_t e : frames.front()) s->event_pool.push_back(e);
+    frames.erase(frames.begin());
+  }
+  std::vector<hipEvent_t> f;
+  while (f.size() < n) {
+    if (!s->event_pool.empty()) {
+      f.push_back(s->event_pool.back());
+      s->event_pool.pop_back();
+    } else {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+      f.push_back(e);
+    }
+  }
+  frames.push_back(std::move(f));
+  *out = &frames.back();
+  return YART_OK;
+}
+
 static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream) {
   const Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
+  std::vector<hipEvent_t>* ev = nullptr;
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
+    if (int rc = timing_events(s, stream, 2, &ev)) return rc;
+    HIP_TRY(hipEventRecord((*ev)[0], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, a, stats, stream), "launch k_render");
+    HIP_TRY(hipEventRecord((*ev)[1], stream), "hipEventRecord");
     return YART_OK;
   }
   double* scratch = nullptr;
   if (int rc = get_scratch(s, stream, (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double), &scratch)) return rc;
-  for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp) {
+  const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
+  if (int rc = timing_events(s, stream, 3 * (size_t)passes, &ev)) return rc;
+  uint32_t k = 0;
+  for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp, ++k) {
     RenderArgs b = a;
     b.s_begin = s0;
     b.s_count = a.spp - s0 < pl.pass_spp ? a.spp - s0 : pl.pass_spp;
     b.chunk = pl.chunk;
     b.n_chunks = (b.s_count + pl.chunk - 1) / pl.chunk;
     b.scratch = scratch;
+    HIP_TRY(hipEventRecord((*ev)[3 * k], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
+    HIP_TRY(hipEventRecord((*ev)[3 * k + 1], stream), "hipEventRecord");
     HIP_TRY(launch_accumulate(b, s0 == 0, stream), "launch k_accumulate");
+    HIP_TRY(hipEventRecord((*ev)[3 * k + 2], stream), "hipEventRecord");
   }
   return YART_OK;
+}
+
+int yart_frame_timing(yart_scene* s, void* stream, double* render_ms, double* accumulate_ms, uint32_t* frames) {
+  if (!s || !render_ms || !accumulate_ms || !frames) return fail(YART_ERR_INVALID, "null argument");
+  DeviceGuard g(s->device);
+  std::lock_guard<std::mutex> lk(s->scratch_mu);
+  auto it = s->frames.find((hipStream_t)stream);
+  double r = 0.0, acc = 0.0;
+  uint32_t n_frames = 0;
+  if (it != s->frames.end()) {
+    for (const auto& v : it->second) {
+      float ms = 0.0f;
+      if (v.size() == 2) {
+        HIP_TRY(hipEventElapsedTime(&ms, v[0], v[1]), "hipEventElapsedTime");
+        r += ms;
+      } else {
+        for (size_t k = 0; k + 2 < v.size(); k += 3) {
+          HIP_TRY(hipEventElapsedTime(&ms, v[k], v[k + 1]), "hipEventElapsedTime");
+          r += ms;
+          HIP_TRY(hipEventElapsedTime(&ms, v[k + 1], v[k + 2]), "hipEventElapsedTime");
+          acc += ms;
+        }
+      }
+      ++n_frames;
+    }
+    for (auto& v : it->second)
+      for (hipEvent_t e : v) s->event_pool.push_back(e);
+    it->second.clear();
+  }
+  *render_ms = r;
+  *accumulate_ms = acc;
+  *frames = n_frames;
+  return ok();
 }
 
 int yart_render_async(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* d_xyz_sum,

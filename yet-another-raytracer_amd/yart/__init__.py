@@ -83,6 +83,7 @@ def load_device():
     _sig(L, "yart_scene_get_info", I, P, C.POINTER(abi.SceneInfo))
     _sig(L, "yart_camera_init", I, C.POINTER(abi.Camera), P, P, P, D, D, D, D, D, D)
     _sig(L, "yart_render_async", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, P)
+    _sig(L, "yart_frame_timing", I, P, P, C.POINTER(D), C.POINTER(D), C.POINTER(U32))
     _sig(L, "yart_render", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, abi.PROGRESS_FN, P)
     _sig(L, "yart_render_with_stats", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P,
          C.POINTER(abi.RenderStats))
@@ -199,6 +200,13 @@ class DeviceScene:
     def render_async(self, cam, params, d_xyz_ptr, stream_ptr):
         _check_dev(load_device().yart_render_async(self._s, C.byref(cam), C.byref(params), C.c_void_p(d_xyz_ptr),
                                                   C.c_void_p(stream_ptr)))
+
+    def frame_timing(self, stream_ptr):
+        """(render_ms, accumulate_ms, frames): summed kernel times of the frames launched on that
+        stream since the last call (HIP events on the stream)."""
+        r, a, n = C.c_double(), C.c_double(), C.c_uint32()
+        _check_dev(load_device().yart_frame_timing(self._s, C.c_void_p(stream_ptr), C.byref(r), C.byref(a), C.byref(n)))
+        return r.value, a.value, n.value
 
     def intersect(self, rays):
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
