@@ -126,8 +126,15 @@ static inline double powi5(double x) { double x2 = x * x; return x * (x2 * x2); 
 
 /* ------------------------------------------------------------------------ RNG
  * Philox4x32-10 (Salmon et al., SC'11; Random123) keyed by the 64-bit seed, counter
- * (block, sample, pixel, stream). Each block yields two u64 draws. The mappings from u64 to
- * the values the reference asks rand 0.8.5 for are restated below. */
+ * (block, sample, pixel, phase << 1 | stream). Each block yields two u64 draws, taken in order.
+ * A path's draws are split into phases, each with its own run of blocks from block 0: phase 0
+ * is the camera ray (main.rs:692-698), phase k >= 1 the scatter at the k-th bounce
+ * (max_depth - depth + 1 of ray_reflectance main.rs:537). The reference draws from
+ * rand::thread_rng, whose stream is not reproducible, so the stream layout is this
+ * implementation's own; phases let the GPU compute each bounce's blocks at one place in its
+ * loop. Draws whose value cannot reach any output are not taken (a one-element index range,
+ * the ray time no in-scope object reads). The mappings from u64 to the values the reference
+ * asks rand 0.8.5 for are restated below. */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
   for (int i = 0; i < 10; ++i) {
@@ -144,6 +151,10 @@ typedef struct { uint32_t key[2]; uint32_t ctr[4]; uint32_t buf[4]; int have; } 
 static void rng_init(rng_t* r, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
   r->key[0] = (uint32_t)seed; r->key[1] = (uint32_t)(seed >> 32);
   r->ctr[0] = 0; r->ctr[1] = sample; r->ctr[2] = pixel; r->ctr[3] = stream;
+  r->have = 0;
+}
+static void rng_phase(rng_t* r, uint32_t phase) {
+  r->ctr[0] = 0; r->ctr[3] = (phase << 1) | (r->ctr[3] & 1u);
   r->have = 0;
 }
 static inline uint64_t rng_u64(rng_t* r) {
@@ -167,6 +178,7 @@ static inline double gen_range_f64(rng_t* r, double low, double high) {
 }
 /* rand 0.8.5 UniformInt<usize>::sample_single(0..n): widening multiply, zone rejection. */
 static inline uint64_t gen_range_usize(rng_t* r, uint64_t n) {
+  if (n == 1) return 0; /* the only value; its rejection draws are unobservable */
   uint64_t range = n;
   uint64_t zone = (range << __builtin_clzll(range)) - 1;
   for (;;) {
@@ -792,7 +804,7 @@ static ray_t camera_get_ray(const yart_camera* c, double s, double t, double wl,
   ray_t r;
   r.o = vadd(org, offset);
   r.d = vsub(vsub(vadd(vadd(llc, smulv(s, hor)), smulv(t, ver)), org), offset);
-  r.time = gen_range_f64(g, c->time0, c->time1);
+  r.time = c->time0; /* gen_range(time0..time1) in camera.rs:92; no in-scope object reads it */
   r.wl = wl;
   return r;
 }
@@ -802,8 +814,9 @@ static ray_t camera_get_ray(const yart_camera* c, double s, double t, double wl,
  * 1 pdf branch (R = att * next * spdf / pdf). */
 typedef struct { int cont; int kind; double att, spdf, pdf; double terminal; ray_t next; } bounce_t;
 
-static void bounce(const oracle_scene* s, const ray_t* r, rng_t* g, bounce_t* b) {
+static void bounce(const oracle_scene* s, const ray_t* r, rng_t* g, uint32_t phase, bounce_t* b) {
   hit_rec rec;
+  rng_phase(g, phase);
   b->cont = 0;
   if (!world_hit(s, r, 0.001, INFINITY, &rec, NULL)) {
     b->terminal = oracle_rgb_reflect(s->background, r->wl); /* main.rs:587 */
@@ -866,23 +879,25 @@ static void bounce(const oracle_scene* s, const ray_t* r, rng_t* g, bounce_t* b)
   }
 }
 
-static double reflectance_recursive(const oracle_scene* s, const ray_t* r, rng_t* g, uint32_t depth) { /* main.rs:537-588 */
+static double reflectance_recursive(const oracle_scene* s, const ray_t* r, rng_t* g, uint32_t depth,
+                                    uint32_t max_depth) { /* main.rs:537-588 */
   if (depth == 0) return 1.0;
   bounce_t b;
-  bounce(s, r, g, &b);
+  bounce(s, r, g, max_depth - depth + 1, &b);
   if (!b.cont) return b.terminal;
-  if (b.kind == 0) return b.att * reflectance_recursive(s, &b.next, g, depth - 1);
-  return b.att * reflectance_recursive(s, &b.next, g, depth - 1) * b.spdf / b.pdf;
+  if (b.kind == 0) return b.att * reflectance_recursive(s, &b.next, g, depth - 1, max_depth);
+  return b.att * reflectance_recursive(s, &b.next, g, depth - 1, max_depth) * b.spdf / b.pdf;
 }
 /* The same recursion unrolled front to back: T accumulates att (and * spdf / pdf); the
  * terminal value multiplies last. Equal to the recursive form up to rounding order. */
 static double reflectance_iterative(const oracle_scene* s, const ray_t* r0, rng_t* g, uint32_t depth) {
+  const uint32_t max_depth = depth;
   double T = 1.0;
   ray_t r = *r0;
   for (;;) {
     if (depth == 0) return T * 1.0;
     bounce_t b;
-    bounce(s, &r, g, &b);
+    bounce(s, &r, g, max_depth - depth + 1, &b);
     if (!b.cont) return T * b.terminal;
     if (b.kind == 0) T = T * b.att;
     else T = ((T * b.att) * b.spdf) / b.pdf;
@@ -930,7 +945,7 @@ static void render_pixel(const job_t* j, uint32_t x, uint32_t y) {
     double v = 1.0 - ty / (double)(H - 1);
     double wl = gen_range_f64(&g, MIN_LAMBDA, MAX_LAMBDA); /* color.rs:20-23 */
     ray_t r = camera_get_ray(j->cam, u, v, wl, &g);
-    double R = j->mode ? reflectance_recursive(j->s, &r, &g, p->max_depth)
+    double R = j->mode ? reflectance_recursive(j->s, &r, &g, p->max_depth, p->max_depth)
                        : reflectance_iterative(j->s, &r, &g, p->max_depth);
     double cie[3], xyz[3], san[3];
     oracle_xyz_from_wavelength(r.wl, cie); /* ray_color main.rs:526-535 */

@@ -105,6 +105,37 @@ def test_intersect_matches_oracle(dev, scene):
     _hits_equal(h, o, h2, o2)
 
 
+def test_box_cull_is_exact_on_grazing_rays(dev):
+    """The device's f32 box pre-test may only skip boxes no face of which is hit: rays aimed at
+    box edges and corners, nudged by a few ulps to tiny offsets, must hit exactly as the oracle."""
+    b = O.DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    b.obj(abi.PRIM_BOX, m, (130.0, 0.0, 65.0, 295.0, 165.0, 230.0))
+    b.obj(abi.PRIM_BOX, m, (0.0, 0.0, 0.0, 165.0, 330.0, 165.0),
+          xforms=[(abi.XF_TRANSLATE, (265.0, 0.0, 295.0)), (abi.XF_ROTATE_Y, (15.0, 0.0, 0.0))])
+    b.obj(abi.PRIM_BOX, m, (-1e-3, -2e-3, -1e-3, 1e-3, 2e-3, 1e-3), xforms=[(abi.XF_TRANSLATE, (400.0, 5.0, 50.0))])
+    d = b.desc()
+    rng = np.random.default_rng(21)
+    n = 120000
+    corners = np.array([[x, y, z] for x in (130.0, 295.0) for y in (0.0, 165.0) for z in (65.0, 230.0)])
+    tgt = corners[rng.integers(0, 8, n)]
+    # slide along a random edge direction, then nudge off the surface by 0..1e-9 relative
+    edge = np.eye(3)[rng.integers(0, 3, n)] * rng.uniform(0, 165, (n, 1))
+    tgt = tgt + edge * np.where(rng.random((n, 1)) < 0.5, 0.0, 1.0)
+    tgt = tgt * (1.0 + rng.choice([-1.0, 0.0, 1.0], (n, 3)) * 10.0 ** rng.uniform(-16, -9, (n, 3)))
+    tiny = np.array([400.0, 5.0, 50.0]) + rng.uniform(-2e-3, 2e-3, (20000, 3))
+    tgt = np.concatenate([tgt, tiny])
+    org = rng.uniform(-600, 1200, (tgt.shape[0], 3))
+    dirs = (tgt - org) * rng.choice([1.0, 1e-3, 1e3], (tgt.shape[0], 1))
+    rays = np.concatenate([org, dirs, np.full((len(org), 1), 0.001), np.full((len(org), 1), np.inf)], axis=1)
+    rays[::7, 7] = rng.uniform(0.5, 2.0, len(rays[::7])) * np.linalg.norm(tgt - org, axis=1)[::7] / \
+        np.linalg.norm(dirs, axis=1)[::7]  # finite t_max around the hit distance
+    h, o = yart.DeviceScene(d).intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    assert (o >= 0).mean() > 0.2
+    _hits_equal(h, o, h2, o2)
+
+
 def test_scene_info_matches_reference_qbvh(dev):
     p = yart.Preset("david")
     s = yart.DeviceScene(p)

@@ -97,13 +97,22 @@ __device__ __forceinline__ double sin_det(double x) { double s, c; sincos_det(x,
 __device__ __forceinline__ double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }  // material.rs:210
 
 // ---------------------------------------------------------------- RNG (Philox4x32-10)
-struct Rng { uint32_t k0, k1, c0, c1, c2, c3, b0, b1, b2, b3; int have; };
+// Counter (block, sample, pixel, phase << 1 | stream), key = seed; oracle.c states the stream
+// layout. A path's draws come in phases — phase 0 the camera ray, phase k the scatter at the k-th
+// bounce — each starting at block 0, so k_render computes an iteration's first two blocks at
+// ONE place for the whole wave (rng_phase) instead of at every draw site any lane reaches with
+// an empty buffer. The buffer is consumed by shifting, which in straight-line code is register
+// renaming; a draw past the fourth refills in place (rare: rejection loops).
+struct Rng { uint32_t k0, k1, c0, c1, c2, c3, b0, b1, b2, b3, b4, b5, b6, b7; int have; };
 __device__ __forceinline__ void rng_init(Rng& r, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
   r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32);
   r.c0 = 0; r.c1 = sample; r.c2 = pixel; r.c3 = stream; r.have = 0;
 }
-__device__ __forceinline__ void philox(Rng& r) {
-  uint32_t c0 = r.c0, c1 = r.c1, c2 = r.c2, c3 = r.c3, k0 = r.k0, k1 = r.k1;
+#ifdef YART_ATTR
+__device__ __forceinline__ uint32_t opaque_zero() { uint32_t z; asm volatile("v_mov_b32 %0, 0" : "=v"(z)); return z; }
+#endif
+__device__ __forceinline__ void philox(const Rng& r, uint32_t blk, uint32_t& o0, uint32_t& o1, uint32_t& o2, uint32_t& o3) {
+  uint32_t c0 = blk, c1 = r.c1, c2 = r.c2, c3 = r.c3, k0 = r.k0, k1 = r.k1;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -111,11 +120,19 @@ __device__ __forceinline__ void philox(Rng& r) {
     c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
-  r.b0 = c0; r.b1 = c1; r.b2 = c2; r.b3 = c3;
+  o0 = c0; o1 = c1; o2 = c2; o3 = c3;
+}
+// Start `phase` of (pixel, sample) with blocks 0 and 1 in the buffer (4 draws).
+__device__ __forceinline__ void rng_phase(Rng& r, uint32_t pixel, uint32_t sample, uint32_t phase) {
+  r.c1 = sample; r.c2 = pixel; r.c3 = phase << 1;
+  philox(r, 0u, r.b0, r.b1, r.b2, r.b3);
+  philox(r, 1u, r.b4, r.b5, r.b6, r.b7);
+  r.c0 = 2; r.have = 4;
 }
 __device__ __forceinline__ uint64_t rng_u64(Rng& r) {
-  if (r.have == 0) { philox(r); r.c0++; r.have = 2; }
-  uint64_t v = (r.have == 2) ? (((uint64_t)r.b1 << 32) | r.b0) : (((uint64_t)r.b3 << 32) | r.b2);
+  if (r.have == 0) { philox(r, r.c0, r.b0, r.b1, r.b2, r.b3); r.c0++; r.have = 2; }
+  const uint64_t v = ((uint64_t)r.b1 << 32) | r.b0;
+  r.b0 = r.b2; r.b1 = r.b3; r.b2 = r.b4; r.b3 = r.b5; r.b4 = r.b6; r.b5 = r.b7;
   r.have--;
   return v;
 }
@@ -131,6 +148,7 @@ __device__ __forceinline__ double gen_range(Rng& r, double low, double high) {  
   return low;
 }
 __device__ __forceinline__ uint64_t gen_index(Rng& r, uint64_t n) {  // UniformInt<usize> 0..n
+  if (n == 1) return 0;  // the only value; its rejection draws are unobservable (oracle.c)
   uint64_t zone = (n << __clzll(n)) - 1;
   for (int guard = 0; guard < 64; ++guard) {
     uint64_t v = rng_u64(r);
@@ -200,7 +218,42 @@ __device__ __forceinline__ bool xy_hit(const double* p, const Ray& r, double a, 
 __device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<1, 0, 2>(p, r, a, b, h); }
 __device__ __forceinline__ bool yz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<0, 1, 2>(p, r, a, b, h); }
 
+// Conservative f32 slab pre-test for BoxEntity (not in the reference; exact by construction): a
+// face hit's computed point lies within a few f64 ulps of the box, so a ray whose parameter
+// range misses the box grown by m = 2^-12 (|box| + |origin|) cannot hit any face, and the six f64
+// face tests may be skipped. f32 rounding (~1e-7 relative) stays far inside m; rays with
+// non-finite components, or a direction component too small for f32, are never culled.
+__device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
+#ifdef YART_NO_BOX_CULL
+  return true;
+#else
+  const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
+  const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
+  const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
+  if (!(fabsf(chk) <= 3.0e38f)) return true;  // NaN / inf / near-overflow: do not cull
+  const float bmn[3] = {fminf((float)p[0], (float)p[3]), fminf((float)p[1], (float)p[4]), fminf((float)p[2], (float)p[5])};
+  const float bmx[3] = {fmaxf((float)p[0], (float)p[3]), fmaxf((float)p[1], (float)p[4]), fmaxf((float)p[2], (float)p[5])};
+  const float B = fmaxf(fmaxf(fmaxf(fabsf(bmn[0]), fabsf(bmn[1])), fmaxf(fabsf(bmn[2]), fabsf(bmx[0]))),
+                        fmaxf(fabsf(bmx[1]), fabsf(bmx[2])));
+  const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
+  const float m = (B + O) * 0x1p-12f;
+  float lo = (float)tmin, hi = (float)tmax;
+  lo = lo - fabsf(lo) * 0x1p-10f;
+  hi = hi + fabsf(hi) * 0x1p-10f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (!(fabsf(d[j]) >= 1.0e-20f)) continue;  // slab unconstrained
+    const float inv = __builtin_amdgcn_rcpf(d[j]);
+    const float t0 = (bmn[j] - m - o[j]) * inv, t1 = (bmx[j] + m - o[j]) * inv;
+    lo = fmaxf(lo, fminf(t0, t1));
+    hi = fminf(hi, fmaxf(t0, t1));
+  }
+  return lo <= hi;
+#endif
+}
+
 __device__ __forceinline__ bool box_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // box_entity.rs:53-70
+  if (!box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
   double closest = tmax;
   Hit tmp;
@@ -507,7 +560,7 @@ __device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double
   Ray r;
   r.o = add(org, offset);
   r.d = sub(sub(add(add(ld3(c.lower_left_corner), smul(s, ld3(c.horizontal))), smul(t, ld3(c.vertical))), org), offset);
-  r.time = gen_range(g, c.time0, c.time1);
+  r.time = c.time0;  // gen_range(time0..time1) (camera.rs:92): no in-scope object reads it
   r.wl = wl;
   return r;
 }
@@ -574,6 +627,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
   double T = 1.0;
   uint32_t depth = 0;
   bool fresh = !DYN && alive;  // start a sample at the top of the loop
+  V3 hp = mk(0.0, 0.0, 0.0), hn = hp;  // the hit to scatter at the top of the next iteration
+  uint32_t hmat = 0;
+  g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
 
   while (alive) {
     if (DYN) {
@@ -596,8 +652,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
       if (!alive) break;
       if (need) continue;  // the job's pixel is outside the crop grid: take another
     }
+    // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
+    // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
+    // found (phase max_depth - depth + 1, its bounce level).
+    rng_phase(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
+    double R = 0.0;
+    bool term = false;
     if (fresh) {  // main.rs:692-698
-      rng_init(g, A.seed, pixel, smp, 0);
       const double tx = (double)x + gen_f64(g);
       const double u = tx / (double)(W - 1);
       const double ty = (double)y + gen_f64(g);
@@ -607,102 +668,116 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
       T = 1.0;
       depth = A.max_depth;
       fresh = false;
+    } else {  // scatter at the stored hit (material.rs), main.rs:548-584
+      const DevMaterial& m = S.materials[hmat];
+      const uint32_t kind = m.kind;
+      if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+        const double att = texture_value(S, m.texture, ray.wl, hp);
+        const Onb uvw = onb_from_w(hn);
+        V3 dir;
+        double pdf_val;
+        if (S.n_lights == 0) {
+          (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
+          dir = local(uvw, random_cosine_direction(g));
+          pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
+        } else {
+          if (gen_range(g, 0.0, 1.0) < 0.5) {
+            // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+            const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+            dir = light_random(S.lights[k], hp, g);
+          } else {
+            dir = local(uvw, random_cosine_direction(g));
+          }
+          const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+          double sum = -0.0;
+          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st);
+          pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
+        }
+        if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+          R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+          term = true;
+        } else {
+          const double cosine = dot(hn, unit(dir));  // Lambertian::scatter_pdf
+          const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+          T = ((T * att) * spdf) / pdf_val;
+          ray.o = hp;
+          ray.d = dir;
+          depth--;
+        }
+      } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+        const V3 reflected = reflect(unit(ray.d), hn);
+        V3 p;
+        for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+          const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+          p = mk(px, py, pz);
+          if (!(len2(p) >= 1.0)) break;
+        }
+        const double att = texture_value(S, m.texture, ray.wl, hp);
+        T = T * att;
+        ray.o = hp;
+        ray.d = add(reflected, smul(m.fuzz, p));
+        depth--;
+      } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+        const double wl2 = ray.wl * ray.wl;
+        const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+        const double n = sqrt(n2);
+        V3 outward;
+        double ni_over_nt, cosine;
+        if (dot(ray.d, hn) > 0.0) {
+          outward = neg(hn); ni_over_nt = n; cosine = n * dot(ray.d, hn) / len(ray.d);
+        } else {
+          outward = hn; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, hn) / len(ray.d);
+        }
+        const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
+        const double dt = dot(uv, outward);
+        const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+        V3 out;
+        if (disc > 0.0) {
+          const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
+          double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+          r0 = r0 * r0;
+          const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+          out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
+        } else {
+          out = reflect(ray.d, hn);
+        }
+        T = T * 1.0;
+        ray.o = hp;
+        ray.d = out;
+        depth--;
+      }
     }
-    double R = 0.0;
-    bool term = false;
-    if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
-      R = T * 1.0;
-      term = true;
-    } else {
-      Hit h;
-      int32_t which;
-      if (STATS) st.v[ST_SEGMENTS]++;
-      if (!world_hit<HAS_MESH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
-        const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
-        R = T * S.background[bin];
+    if (!term) {
+      if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
+        R = T * 1.0;
         term = true;
       } else {
-        const DevMaterial& m = S.materials[h.mat];
-        const uint32_t kind = m.kind;
-        if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-          const double att = texture_value(S, m.texture, ray.wl, h.p);
-          const Onb uvw = onb_from_w(h.n);
-          V3 dir;
-          double pdf_val;
-          if (S.n_lights == 0) {
-            (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
-            dir = local(uvw, random_cosine_direction(g));
-            pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
-          } else {
-            if (gen_range(g, 0.0, 1.0) < 0.5) {
-              // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
-              const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
-              dir = light_random(S.lights[k], h.p, g);
-            } else {
-              dir = local(uvw, random_cosine_direction(g));
-            }
-            const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-            double sum = -0.0;
-            for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], h.p, dir, ray.wl, st);
-            pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
-          }
-          if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-            R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-            term = true;
-          } else {
-            const double cosine = dot(h.n, unit(dir));  // Lambertian::scatter_pdf
-            const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-            T = ((T * att) * spdf) / pdf_val;
-            ray.o = h.p;
-            ray.d = dir;
-            depth--;
-          }
-        } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
-          const V3 reflected = reflect(unit(ray.d), h.n);
-          V3 p;
-          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-            p = mk(px, py, pz);
-            if (!(len2(p) >= 1.0)) break;
-          }
-          const double att = texture_value(S, m.texture, ray.wl, h.p);
-          T = T * att;
-          ray.o = h.p;
-          ray.d = add(reflected, smul(m.fuzz, p));
-          depth--;
-        } else if (kind == YART_MAT_DIELECTRIC) {  // material.rs:213-301
-          const double wl2 = ray.wl * ray.wl;
-          const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-          const double n = sqrt(n2);
-          V3 outward;
-          double ni_over_nt, cosine;
-          if (dot(ray.d, h.n) > 0.0) {
-            outward = neg(h.n); ni_over_nt = n; cosine = n * dot(ray.d, h.n) / len(ray.d);
-          } else {
-            outward = h.n; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, h.n) / len(ray.d);
-          }
-          const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
-          const double dt = dot(uv, outward);
-          const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
-          V3 out;
-          if (disc > 0.0) {
-            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
-            double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
-            r0 = r0 * r0;
-            const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
-            out = gen_f64(g) < sch ? reflect(ray.d, h.n) : refracted;
-          } else {
-            out = reflect(ray.d, h.n);
-          }
-          T = T * 1.0;
-          ray.o = h.p;
-          ray.d = out;
-          depth--;
-        } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
-          double emitted = 0.0;
-          if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value(S, m.texture, ray.wl, h.p);
-          R = T * emitted;
+        Hit h;
+        int32_t which;
+        if (STATS) st.v[ST_SEGMENTS]++;
+#ifdef YART_ATTR_WORLD2
+        {
+          Hit h2; int32_t w2;
+          const uint32_t z = opaque_zero();
+          Ray r2 = ray; r2.o.x = r2.o.x + (double)z;
+          if (world_hit<HAS_MESH, STATS>(S, r2, 0.001, INFINITY, h2, w2, stk, st) && z) A.out[w2] = h2.t;
+        }
+#endif
+        if (!world_hit<HAS_MESH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
+          const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
+          R = T * S.background[bin];
           term = true;
+        } else {
+          const DevMaterial& m = S.materials[h.mat];
+          const uint32_t kind = m.kind;
+          if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC) {
+            hp = h.p; hn = h.n; hmat = h.mat;  // scattered at the top of the next iteration
+          } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
+            double emitted = 0.0;
+            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value(S, m.texture, ray.wl, h.p);
+            R = T * emitted;
+            term = true;
+          }
         }
       }
     }
