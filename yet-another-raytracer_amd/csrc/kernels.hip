@@ -174,7 +174,10 @@ __device__ __forceinline__ void cie_xyz(double wl, double& x, double& y, double&
 }
 
 // ------------------------------------------------------------------- primitive hits
-__device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // sphere.rs:48-86
+// Each primitive comes as a closest-hit test that only finds t (`*_t`) and a record builder
+// (`*_rec`) run once for the winning primitive of a world query; `*_hit` is the two together.
+// Split or not, every value is computed by the same expression on the same inputs.
+__device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {  // sphere.rs:48-86
   V3 center = mk(p[0], p[1], p[2]);
   double radius = p[3];
   V3 oc = sub(r.o, center);
@@ -184,39 +187,58 @@ __device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double
   double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
   double sq = sqrt(disc);
-  double t = (0.0 - half_b - sq) / a;
+  t = (0.0 - half_b - sq) / a;
   if (t < tmin || tmax < t) {
     t = (0.0 - half_b + sq) / a;
     if (t < tmin || tmax < t) return false;
   }
+  return true;
+}
+__device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h) {
+  V3 center = mk(p[0], p[1], p[2]);
+  double radius = p[3];
   V3 pt = at(r, t);
   V3 outward = divs(sub(pt, center), fabs(radius));
   if (radius < 0.0) { h.n = neg(outward); h.ff = dot(r.d, outward) > 0.0; }
   else { h.n = outward; h.ff = dot(r.d, outward) < 0.0; }
   h.t = t; h.p = pt;
+}
+__device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
+  double t;
+  if (!sphere_t(p, r, tmin, tmax, t)) return false;
+  sphere_rec(p, r, t, h);
   return true;
 }
 
 // aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
 template <int A, int B, int CC>
-__device__ __forceinline__ bool rect_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
+__device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
-  double t = num / den;
+  t = num / den;
   if (t < tmin || t > tmax) return false;
   double x = o[B] + t * d[B];
   double y = o[CC] + t * d[CC];
   if (x < p[0] || x > p[1] || y < p[2] || y > p[3]) return false;
-  V3 outward = mk(A == 0 ? 1.0 : 0.0, A == 1 ? 1.0 : 0.0, A == 2 ? 1.0 : 0.0);
+  return true;
+}
+// Record of an axis-aligned rect with plane axis `a` (0 yz, 1 xz, 2 xy); a runtime axis lets the
+// rect and box-face records of a wave share one code path.
+__device__ __forceinline__ void rect_rec(uint32_t a, const Ray& r, double t, Hit& h) {
+  V3 outward = mk(a == 0 ? 1.0 : 0.0, a == 1 ? 1.0 : 0.0, a == 2 ? 1.0 : 0.0);
   h.t = t; h.p = at(r, t);
   if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
   else { h.n = neg(outward); h.ff = false; }
+}
+template <int A, int B, int CC>
+__device__ __forceinline__ bool rect_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
+  double t;
+  if (!rect_t<A, B, CC>(p, r, tmin, tmax, t)) return false;
+  rect_rec(A, r, t, h);
   return true;
 }
-__device__ __forceinline__ bool xy_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<2, 0, 1>(p, r, a, b, h); }
 __device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<1, 0, 2>(p, r, a, b, h); }
-__device__ __forceinline__ bool yz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<0, 1, 2>(p, r, a, b, h); }
 
 // Conservative f32 slab pre-test for BoxEntity (not in the reference; exact by construction): a
 // face hit's computed point lies within a few f64 ulps of the box, so a ray whose parameter
@@ -252,25 +274,28 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
 #endif
 }
 
-__device__ __forceinline__ bool box_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // box_entity.rs:53-70
+// BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
+// 4-5 yz, so the face's plane axis is 2 - face / 2.
+__device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face) {
   if (!box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
-  double closest = tmax;
-  Hit tmp;
+  double closest = tmax, tt;
   double s[5];
   s[0] = p[0]; s[1] = p[3]; s[2] = p[1]; s[3] = p[4];
-  s[4] = p[2]; if (xy_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
-  s[4] = p[5]; if (xy_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[2]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 0; found = true; }
+  s[4] = p[5]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 1; found = true; }
   s[2] = p[2]; s[3] = p[5];
-  s[4] = p[1]; if (xz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
-  s[4] = p[4]; if (xz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[1]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 2; found = true; }
+  s[4] = p[4]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 3; found = true; }
   s[0] = p[1]; s[1] = p[4];
-  s[4] = p[0]; if (yz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
-  s[4] = p[3]; if (yz_hit(s, r, tmin, closest, tmp)) { closest = tmp.t; h = tmp; found = true; }
+  s[4] = p[0]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 4; found = true; }
+  s[4] = p[3]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 5; found = true; }
+  t = closest;
   return found;
 }
 
-__device__ __forceinline__ bool triangle_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {  // triangle.rs:48-101
+__device__ __forceinline__ bool triangle_t(const double* p, const Ray& r, double tmin, double tmax, double& t,
+                                           double& u, double& v) {  // triangle.rs:48-101
   V3 v0 = ld3(p), v1 = ld3(p + 3), v2 = ld3(p + 6);
   V3 e1 = sub(v1, v0), e2 = sub(v2, v0);
   V3 hh = cross(r.d, e2);
@@ -278,19 +303,21 @@ __device__ __forceinline__ bool triangle_hit(const double* p, const Ray& r, doub
   if (a > -kEps && a < kEps) return false;
   double f = 1.0 / a;
   V3 s = sub(r.o, v0);
-  double u = f * dot(s, hh);
+  u = f * dot(s, hh);
   if (u < 0.0 || u > 1.0) return false;
   V3 q = cross(s, e1);
-  double v = f * dot(r.d, q);
+  v = f * dot(r.d, q);
   if (v < 0.0 || u + v > 1.0) return false;
-  double t = f * dot(e2, q);
+  t = f * dot(e2, q);
   if (t < tmin || t > tmax) return false;
+  return true;
+}
+__device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, double t, double u, double v, Hit& h) {
   double w = 1.0 - u - v;
   V3 outward = add(add(muls(ld3(p + 9), w), muls(ld3(p + 12), u)), muls(ld3(p + 15), v));
   h.t = t; h.p = at(r, t);
   if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
   else { h.n = neg(outward); h.ff = false; }
-  return true;
 }
 
 // --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543), per lane
@@ -298,8 +325,8 @@ struct Stats { unsigned long long v[8]; };
 enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };
 
 template <bool STATS>
-__device__ __noinline__ bool qbvh_hit(const DevMesh& M, const Ray& r, double tmin, double tmax, Hit& h,
-                                      uint32_t* __restrict__ stk, Stats& st) {
+__device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin, double tmax, double& t_hit,
+                                    uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st) {
   // ORDER_TABLE (qbvh.rs:14-16), two 16-bit entries per nibble group packed in 64-bit words.
   const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
   const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
@@ -337,18 +364,9 @@ __device__ __noinline__ bool qbvh_hit(const DevMesh& M, const Ray& r, double tmi
         const bool hit = !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 &&
                          t >= tmin && tmax > t;
         if (hit) {
-          const double w = 1.0 - u - v;
-          const double* nn = M.normals + 9 * (size_t)(M.leaf_first[li] + i);
-          const double onx = nn[0] * w + nn[3] * u + nn[6] * v;
-          const double ony = nn[1] * w + nn[4] * u + nn[7] * v;
-          const double onz = nn[2] * w + nn[5] * u + nn[8] * v;
-          const bool ff = (rd[0] * onx + rd[1] * ony + rd[2] * onz) <= 0.0;
-          const double sign = ff ? 1.0 : -1.0;
           tmax = t;
-          h.t = t;
-          h.p = mk(ro[0] + t * rd[0], ro[1] + t * rd[1], ro[2] + t * rd[2]);
-          h.n = mk(sign * onx, sign * ony, sign * onz);
-          h.ff = ff;
+          t_hit = t; u_hit = u; v_hit = v;
+          tri = M.leaf_first[li] + i;
           found = true;
         }
       }
@@ -396,73 +414,132 @@ __device__ __noinline__ bool qbvh_hit(const DevMesh& M, const Ray& r, double tmi
   return found;
 }
 
+// The QBVH leaf record (qbvh.rs:500-540): barycentric normal of the winning triangle, facing
+// the ray (front face when dot <= 0).
+__device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double t, uint32_t tri, double u, double v, Hit& h) {
+  const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+  const double w = 1.0 - u - v;
+  const double* nn = M.normals + 9 * (size_t)tri;
+  const double onx = nn[0] * w + nn[3] * u + nn[6] * v;
+  const double ony = nn[1] * w + nn[4] * u + nn[7] * v;
+  const double onz = nn[2] * w + nn[5] * u + nn[8] * v;
+  const bool ff = (rd[0] * onx + rd[1] * ony + rd[2] * onz) <= 0.0;
+  const double sign = ff ? 1.0 : -1.0;
+  h.t = t;
+  h.p = mk(ro[0] + t * rd[0], ro[1] + t * rd[1], ro[2] + t * rd[2]);
+  h.n = mk(sign * onx, sign * ony, sign * onz);
+  h.ff = ff;
+}
+
 // ------------------------------------------------------------------------ world hit
+// Which primitive of the world list won, and where: enough to rebuild its record exactly.
+struct HitId { double t, u, v; uint32_t obj, sub; };
+
 template <bool HAS_MESH, bool STATS>
-__device__ __forceinline__ bool prim_hit(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
-                                         double tmin, double tmax, Hit& h, uint32_t* stk, Stats& st) {
+__device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
+                                       double tmin, double tmax, double& t, uint32_t& sub, double& u, double& v,
+                                       uint32_t* stk, Stats& st) {
   switch (kind) {
-    case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_hit(o.p, r, tmin, tmax, h);
-    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return xy_hit(o.p, r, tmin, tmax, h);
-    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return xz_hit(o.p, r, tmin, tmax, h);
-    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return yz_hit(o.p, r, tmin, tmax, h);
-    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_hit(o.p, r, tmin, tmax, h);
-    case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_hit(o.p, r, tmin, tmax, h);
+    case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_t(o.p, r, tmin, tmax, t);
+    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t(o.p, r, tmin, tmax, t, sub);
+    case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
     case YART_PRIM_MESH:
-      if constexpr (HAS_MESH) return qbvh_hit<STATS>(S.meshes[o.mesh], r, tmin, tmax, h, stk, st);
+      if constexpr (HAS_MESH) return qbvh_t<STATS>(S.meshes[o.mesh], r, tmin, tmax, t, sub, u, v, stk, st);
       return false;
   }
   return false;
 }
 
-// HittableList::hit (hittable.rs:67-79) with each entry's wrappers applied outermost first on
-// the way in (Translate :136-152, RotateY :217-251) and innermost first on the way out.
+// Translate / RotateY on the way in (hittable.rs:136-152, 217-251), outermost first.
+__device__ __forceinline__ Ray to_local(const DevObject& o, uint32_t nxf, const Ray& r) {
+  Ray lr = r;
+  for (uint32_t l = 0; l < nxf; ++l) {
+    const uint32_t k = o.xf_kind[l];
+    if (k == YART_XF_TRANSLATE) {
+      lr.o = sub(lr.o, ld3(o.xf[l]));
+    } else if (k == YART_XF_ROTATE_Y) {
+      const double sn = o.xf[l][0], cs = o.xf[l][1];
+      const V3 ro = lr.o, rdd = lr.d;
+      lr.o.x = cs * ro.x - sn * ro.z;
+      lr.o.z = sn * ro.x + cs * ro.z;
+      lr.d.x = cs * rdd.x - sn * rdd.z;
+      lr.d.z = sn * rdd.x + cs * rdd.z;
+    }
+  }
+  return lr;
+}
+
+// HittableList::hit (hittable.rs:67-79), split in two: the closest-hit search over the list
+// (uniform object index: the objects arrive on the scalar path) keeps only t and the winner's
+// id, and hit_record then builds the one record the reference keeps — the winner's, with its
+// wrappers undone innermost first on the way out. Building a record per candidate instead
+// cost every wave the selects and point/normal arithmetic of each primitive some lane hit.
 template <bool HAS_MESH, bool STATS>
-__device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, Stats& st) {
+__device__ __forceinline__ bool world_closest(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
+                                              uint32_t* stk, Stats& st) {
   bool found = false;
   double closest = tmax;
+  id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
   for (uint32_t i = 0; i < S.n_objects; ++i) {
     const DevObject& o = S.objects[i];
     const uint32_t kind = o.kind, nxf = o.n_xf;
-    Ray lr = r;
-    for (uint32_t l = 0; l < nxf; ++l) {
-      const uint32_t k = o.xf_kind[l];
-      if (k == YART_XF_TRANSLATE) {
-        lr.o = sub(lr.o, ld3(o.xf[l]));
-      } else if (k == YART_XF_ROTATE_Y) {
-        const double sn = o.xf[l][0], cs = o.xf[l][1];
-        const V3 ro = lr.o, rdd = lr.d;
-        lr.o.x = cs * ro.x - sn * ro.z;
-        lr.o.z = sn * ro.x + cs * ro.z;
-        lr.d.x = cs * rdd.x - sn * rdd.z;
-        lr.d.z = sn * rdd.x + cs * rdd.z;
-      }
-    }
-    Hit t;
-    if (prim_hit<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, stk, st)) {
-      for (int l = (int)nxf - 1; l >= 0; --l) {
-        const uint32_t k = o.xf_kind[l];
-        if (k == YART_XF_TRANSLATE) {
-          t.p = add(t.p, ld3(o.xf[l]));
-        } else if (k == YART_XF_ROTATE_Y) {
-          const double sn = o.xf[l][0], cs = o.xf[l][1];
-          const V3 p = t.p, n = t.n;
-          t.p.x = cs * p.x + sn * p.z;
-          t.p.z = -sn * p.x + cs * p.z;
-          t.n.x = cs * n.x + sn * n.z;
-          t.n.z = -sn * n.x + cs * n.z;
-        } else {
-          t.ff = !t.ff;  // FlipFace (hittable.rs:338-349)
-        }
-      }
-      closest = t.t;
-      t.mat = o.material;
-      rec = t;
-      which = (int32_t)i;
+    const Ray lr = to_local(o, nxf, r);
+    double t, u = 0.0, v = 0.0;
+    uint32_t sub = 0;
+    if (prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st)) {
+      closest = t;
+      id.obj = i; id.sub = sub; id.u = u; id.v = v;
       found = true;
     }
   }
+  id.t = closest;
   return found;
+}
+
+template <bool HAS_MESH>
+__device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, const HitId& id, Hit& h) {
+  const DevObject& o = S.objects[id.obj];  // per lane
+  const uint32_t kind = o.kind, nxf = o.n_xf;
+  const Ray lr = to_local(o, nxf, r);
+  if (kind == YART_PRIM_SPHERE) {
+    sphere_rec(o.p, lr, id.t, h);
+  } else if (kind <= YART_PRIM_BOX) {  // rects and box faces
+    const uint32_t a = kind == YART_PRIM_BOX ? 2u - id.sub / 2u : (kind == YART_PRIM_XY_RECT ? 2u : kind == YART_PRIM_XZ_RECT ? 1u : 0u);
+    rect_rec(a, lr, id.t, h);
+  } else if (kind == YART_PRIM_TRIANGLE) {
+    triangle_rec(o.p, lr, id.t, id.u, id.v, h);
+  } else {
+    if constexpr (HAS_MESH) mesh_rec(S.meshes[o.mesh], lr, id.t, id.sub, id.u, id.v, h);
+  }
+  for (int l = (int)nxf - 1; l >= 0; --l) {
+    const uint32_t k = o.xf_kind[l];
+    if (k == YART_XF_TRANSLATE) {
+      h.p = add(h.p, ld3(o.xf[l]));
+    } else if (k == YART_XF_ROTATE_Y) {
+      const double sn = o.xf[l][0], cs = o.xf[l][1];
+      const V3 p = h.p, n = h.n;
+      h.p.x = cs * p.x + sn * p.z;
+      h.p.z = -sn * p.x + cs * p.z;
+      h.n.x = cs * n.x + sn * n.z;
+      h.n.z = -sn * n.x + cs * n.z;
+    } else {
+      h.ff = !h.ff;  // FlipFace (hittable.rs:338-349)
+    }
+  }
+  h.mat = o.material;
+}
+
+template <bool HAS_MESH, bool STATS>
+__device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
+                                          int32_t& which, uint32_t* stk, Stats& st) {
+  HitId id;
+  if (!world_closest<HAS_MESH, STATS>(S, r, tmin, tmax, id, stk, st)) return false;
+  hit_record<HAS_MESH>(S, r, id, rec);
+  which = (int32_t)id.obj;
+  return true;
 }
 
 
