@@ -34,7 +34,7 @@ def main():
     PROF.mkdir(exist_ok=True)
     shutil.copy(OUT / "prof_trace" / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
     summary = {"kernel": kernel, "source": "tools/profile.sh (rocprofv3 --pmc, one counter block per pass)"}
-    for p in ("prof_fetch", "prof_write", "prof_valu", "prof_stall", "prof_mix", "prof_mem"):
+    for p in ("prof_fetch", "prof_write", "prof_valu", "prof_stall", "prof_mix", "prof_mem", "prof_icache"):
         if (OUT / p / "run_counter_collection.csv").exists():
             v, rows = per_launch(p, kernel)
             summary.update(v)
