@@ -73,14 +73,25 @@ def cpu_baseline(preset, cam, w, h, spp, depth, threads):
                       f"{dt:.2f} s on {threads} threads, oracle/ C restatement"}
 
 
-def pmc_traffic():
-    """HBM bytes per render launch from the committed rocprofv3 PMC summary, if present."""
+def pmc_summary():
+    """The committed rocprofv3 PMC summary of the render kernel (tools/profile.sh), if present."""
     p = ROOT / "profiles" / "pmc_render_cornell.json"
     if not p.exists():
-        return None
+        return {}
     try:
-        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+        return json.loads(p.read_text())
     except Exception:
+        return {}
+
+
+def valu_issue(pmc):
+    """Fraction of SIMD cycles with a VALU instruction executing: SQ_ACTIVE_INST_VALU counts
+    quad-cycles per wave, summed over the chip's 1,024 SIMDs; GRBM_GUI_ACTIVE is summed over
+    the 8 XCDs."""
+    try:
+        simd_cycles = pmc["GRBM_GUI_ACTIVE"] / 8 * 1024
+        return round(4 * pmc["SQ_ACTIVE_INST_VALU"] / simd_cycles, 4)
+    except (KeyError, ZeroDivisionError):
         return None
 
 
@@ -149,7 +160,8 @@ def main():
         flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
                  st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        traffic = pmc_traffic()
+        pmc = pmc_summary()
+        traffic = pmc.get("hbm_bytes_per_launch")
         roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / F64_VALU_PEAK_TFLOPS, 4), "traffic": traffic,
                     "kernel": "k_render<false,false,true>" if accum_ms > 0 else "k_render<false,false,false>",
@@ -158,7 +170,8 @@ def main():
                     "counts": {"samples": st.samples, "segments": st.segments, "prim_tests": st.prim_tests,
                                "light_tests": st.light_tests, "node_visits": st.node_visits,
                                "leaf_tris": st.leaf_tris},
-                    "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None)}
+                    "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None),
+                    "valu_issue_busy": valu_issue(pmc)}
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
 
