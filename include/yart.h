@@ -177,6 +177,8 @@ typedef struct yart_scene_info {
   uint32_t bvh_max_depth; /* deepest root-to-leaf path in inner nodes                   */
   uint32_t bvh_max_stack; /* traversal stack slots the deepest path can need            */
   uint64_t device_bytes;  /* HBM held by the scene                                      */
+  uint32_t world_nodes;   /* world BVH nodes over the object list (0 = linear walk)     */
+  uint32_t world_depth;   /* its deepest root-to-leaf path                              */
 } yart_scene_info;
 
 /* Per-launch work counters (optional, for roofline accounting; they slow the kernel). */

@@ -136,6 +136,55 @@ def test_box_cull_is_exact_on_grazing_rays(dev):
     _hits_equal(h, o, h2, o2)
 
 
+@pytest.mark.parametrize("scene", ["cornell-box", "three-spheres", "two-spheres", "random-scene"])
+def test_world_bvh_forced_on_matches_linear_scan(dev, scene, monkeypatch):
+    """YART_WORLD_BVH=1 puts every boxable list behind the world BVH (wrappers, boxes, flipped
+    light included): closest hits and renders stay bitwise the oracle's linear HittableList."""
+    monkeypatch.setenv("YART_WORLD_BVH", "1")
+    p = yart.Preset(scene)
+    s = yart.DeviceScene(p)
+    assert s.info().world_nodes > 0
+    bounds = {"cornell-box": (0, 555), "three-spheres": (-3, 3), "two-spheres": (-12, 12),
+              "random-scene": (-12, 12)}[scene]
+    rays = _random_rays(100000, *bounds, seed=13)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    _hits_equal(h, o, h2, o2)
+    W, H, spp = 40, 32, 4
+    cam = p.camera(W, H)
+    np.testing.assert_array_equal(s.render(cam, yart.render_params(W, H, spp, 50)),
+                                  O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
+
+
+def test_world_bvh_ties_go_to_the_later_object(dev):
+    """Coincident primitives hit at the same t: the linear scan keeps the LAST one (t == t_max is
+    accepted); the BVH must pick the same object whatever order it visits them in."""
+    b = O.DescBuilder()
+    mats = [b.material(abi.MAT_LAMBERTIAN, b.texture((0.1 * k, 0.5, 0.5))) for k in range(4)]
+    rng = np.random.default_rng(5)
+    for k in range(12):  # 12 positions x 3 coincident copies each, interleaved in list order
+        c = tuple(rng.uniform(-5, 5, 3))
+        for m in range(3):
+            b.obj(abi.PRIM_SPHERE, mats[m], c + (0.7,))
+    for m in range(3):  # three coincident floors, and a box over a rect face
+        b.obj(abi.PRIM_XZ_RECT, mats[m], (-8.0, 8.0, -8.0, 8.0, -6.0))
+    b.obj(abi.PRIM_BOX, mats[3], (-1.0, -6.0, -1.0, 1.0, -5.0, 1.0))
+    b.obj(abi.PRIM_XZ_RECT, mats[2], (-1.0, 1.0, -1.0, 1.0, -5.0))
+    d = b.desc()
+    rays = _random_rays(60000, -9, 9, seed=17)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    for force in ("1", "0"):
+        os_env = {"YART_WORLD_BVH": force}
+        with pytest.MonkeyPatch.context() as mp:
+            for k, v in os_env.items():
+                mp.setenv(k, v)
+            s = yart.DeviceScene(d)
+            assert (s.info().world_nodes > 0) == (force == "1")
+            h, o = s.intersect(rays)
+        assert (o2 >= 0).mean() > 0.15
+        _hits_equal(h, o, h2, o2)
+
+
 def test_scene_info_matches_reference_qbvh(dev):
     p = yart.Preset("david")
     s = yart.DeviceScene(p)

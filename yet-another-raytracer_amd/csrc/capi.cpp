@@ -15,10 +15,15 @@
 #include "../host/camera_impl.h"
 #include "bvh_build.h"
 #include "kernels.h"
+#include "world_bvh.h"
 
 using namespace yart_dev;
 
 namespace {
+
+// Object lists at least this long get a world BVH (the random scene has ~485 spheres; the
+// cornell box's 8 entries are walked linearly).
+constexpr uint32_t kWorldBvhMinObjects = 16;
 
 thread_local std::string g_err;
 int fail(int code, const std::string& m) { g_err = m; return code; }
@@ -206,6 +211,19 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     depth = std::max(depth, built[m].depth);
   }
 
+  // World BVH (world_bvh.h): for long object lists without meshes; YART_WORLD_BVH=0 / 1 forces
+  // the linear walk / the BVH (when every object has a box).
+  BuiltWorld world;
+  bool use_world = false;
+  {
+    bool any_mesh = false;
+    for (uint32_t i = 0; i < d->n_objects; ++i) any_mesh |= d->objects[i].kind == YART_PRIM_MESH;
+    const char* env = std::getenv("YART_WORLD_BVH");
+    const int force = env ? std::atoi(env) : -1;
+    const bool want = force == 1 || (force != 0 && d->n_objects >= kWorldBvhMinObjects);
+    if (want && !any_mesh) use_world = build_world_bvh(objs, world);
+  }
+
   auto s = std::make_unique<yart_scene>();
   s->device = device;
   DeviceGuard guard(device);
@@ -229,6 +247,11 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     dm[m].n_nodes = (uint32_t)b.nodes.size();
   }
   HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
+  if (use_world) {
+    HIP_TRY(upload(s->owned, world.nodes.data(), world.nodes.size(), &ds.world_nodes, bytes), "upload world nodes");
+    HIP_TRY(upload(s->owned, world.objs.data(), world.objs.size(), &ds.world_objs, bytes), "upload world objects");
+    ds.n_world_nodes = (uint32_t)world.nodes.size();
+  }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
   ds.has_mesh = 0;
@@ -239,6 +262,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   in.bvh_nodes = nodes; in.bvh_leaves = leaves; in.bvh_max_depth = depth;
   in.bvh_max_stack = d->n_meshes ? 3 * depth + 1 : 0;
   in.device_bytes = bytes;
+  in.world_nodes = use_world ? (uint32_t)world.nodes.size() : 0;
+  in.world_depth = use_world ? world.depth : 0;
   *out = s.release();
   return ok();
 }

@@ -59,6 +59,20 @@ struct DevMesh {
   uint32_t n_nodes;
 };
 
+// World BVH over the object list (not in the reference, whose HittableList is a linear scan):
+// binary, f32 boxes padded outward so that culling is conservative; children of an inner node
+// are adjacent (first, first + 1); a leaf lists `count` object indices from `first` in
+// DevScene::world_objs. The closest hit it finds is the linear scan's (see world_closest_bvh).
+struct alignas(16) DevWorldNode {
+  float bmin[3];
+  float mag;        // max |coordinate| of the box (margin scale)
+  float bmax[3];
+  uint32_t count;   // 0 = inner node
+  uint32_t first;   // inner: left child (right = first + 1); leaf: first slot in world_objs
+  uint32_t pad[3];
+};
+static_assert(sizeof(DevWorldNode) == 48, "DevWorldNode must be 48 B");
+
 struct DevScene {
   const DevObject* objects;
   const DevObject* lights;
@@ -66,8 +80,11 @@ struct DevScene {
   const DevTexture* textures;
   const DevMesh* meshes;
   const double* background;  // 36 bins
+  const DevWorldNode* world_nodes;  // null: walk the list linearly
+  const uint32_t* world_objs;
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
   uint32_t has_mesh;
+  uint32_t n_world_nodes;
 };
 
 }  // namespace yart_dev

@@ -543,11 +543,107 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
   h.mat = o.material;
 }
 
-template <bool HAS_MESH, bool STATS>
+// World BVH walk (DevWorldNode; scenes without meshes): per lane, near child first, 32-slot
+// stack in LDS like the QBVH. The linear scan accepts an object iff its first root r_i >= t_min
+// satisfies r_i <= closest-so-far (every kind here is inclusive at t_max), so it returns the
+// minimum r_i, ties going to the LATER object; any visiting order that keeps (min t, max index)
+// returns the same winner, and the record is then rebuilt from it as before. Node culling is
+// an f32 slab test against the box grown by m = 2^-12 (node magnitude + |origin|) — f32 rounding
+// (~1e-7 relative) stays far inside m — over [t_min, closest] widened by 2^-10, so it never
+// drops a node holding a hit the scan would accept (ties included). Non-finite rays take the
+// list walk.
+template <bool STATS>
+__device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
+                                                  uint32_t* stk, Stats& st) {
+  const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
+  const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
+  const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
+  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS>(S, r, tmin, tmax, id, stk, st);
+  float inv[3];
+  bool use[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    use[j] = fabsf(d[j]) >= 1.0e-20f;  // smaller: the slab does not constrain t
+    inv[j] = use[j] ? __builtin_amdgcn_rcpf(d[j]) : 0.0f;
+  }
+  const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
+  float tlo = (float)tmin;
+  tlo = tlo - fabsf(tlo) * 0x1p-10f;
+  bool found = false;
+  double closest = tmax;
+  id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
+  uint32_t node = 0;
+  int cursor = 0;
+  for (;;) {
+    const DevWorldNode& N = S.world_nodes[node];
+    const uint32_t count = N.count, first = N.first;
+    bool pop = true;
+    if (count) {
+      for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t i = S.world_objs[first + k];
+        const DevObject& ob = S.objects[i];
+        const Ray lr = to_local(ob, ob.n_xf, r);
+        double t, u = 0.0, v = 0.0;
+        uint32_t sub = 0;
+        if (prim_t<false, STATS>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
+            (!found || t < closest || i > id.obj)) {
+          closest = t;
+          id.obj = i; id.sub = sub; id.u = u; id.v = v;
+          found = true;
+        }
+      }
+    } else {
+      float thi = (float)closest;
+      thi = thi + fabsf(thi) * 0x1p-10f;
+      float entry[2];
+      bool hit[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const DevWorldNode& C = S.world_nodes[first + c];
+        const float m = (C.mag + O) * 0x1p-12f;
+        float lo = tlo, hi = thi;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (use[j]) {
+            const float t0 = (C.bmin[j] - m - o[j]) * inv[j], t1 = (C.bmax[j] + m - o[j]) * inv[j];
+            lo = fmaxf(lo, fminf(t0, t1));
+            hi = fminf(hi, fmaxf(t0, t1));
+          }
+        }
+        entry[c] = lo;
+        hit[c] = lo <= hi;
+      }
+      if (STATS) st.v[ST_NODES]++;
+      if (hit[0] && hit[1]) {
+        const uint32_t near = entry[0] <= entry[1] ? first : first + 1;
+        stk[cursor * 64] = near == first ? first + 1 : first;
+        cursor++;
+        node = near;
+        pop = false;
+      } else if (hit[0] || hit[1]) {
+        node = hit[0] ? first : first + 1;
+        pop = false;
+      }
+    }
+    if (pop) {
+      if (cursor == 0) break;
+      cursor--;
+      node = stk[cursor * 64];
+    }
+  }
+  id.t = closest;
+  return found;
+}
+
+template <bool HAS_MESH, bool BVH, bool STATS>
 __device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
                                           int32_t& which, uint32_t* stk, Stats& st) {
   HitId id;
-  if (!world_closest<HAS_MESH, STATS>(S, r, tmin, tmax, id, stk, st)) return false;
+  if constexpr (BVH) {
+    if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
+  } else {
+    if (!world_closest<HAS_MESH, STATS>(S, r, tmin, tmax, id, stk, st)) return false;
+  }
   hit_record<HAS_MESH>(S, r, id, rec);
   which = (int32_t)id.obj;
   return true;
@@ -678,9 +774,9 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 // wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
 // no lane idles while another still has samples of its own pixel left. Safe because each
 // (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
-template <bool HAS_MESH, bool STATS, bool DYN>
+template <bool HAS_MESH, bool BVH, bool STATS, bool DYN>
 __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
-  __shared__ uint32_t s_stack[HAS_MESH ? 4 * kStackSlots * 64 : 1];
+  __shared__ uint32_t s_stack[(HAS_MESH || BVH) ? 4 * kStackSlots * 64 : 1];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
   // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
@@ -694,7 +790,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
   uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
-  uint32_t* stk = &s_stack[HAS_MESH ? (wave * kStackSlots * 64 + lane) : 0];
+  uint32_t* stk = &s_stack[(HAS_MESH || BVH) ? (wave * kStackSlots * 64 + lane) : 0];
   Stats st;
   if (STATS) for (int i = 0; i < 8; ++i) st.v[i] = 0;
 
@@ -848,10 +944,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_rende
           Hit h2; int32_t w2;
           const uint32_t z = opaque_zero();
           Ray r2 = ray; r2.o.x = r2.o.x + (double)z;
-          if (world_hit<HAS_MESH, STATS>(S, r2, 0.001, INFINITY, h2, w2, stk, st) && z) A.out[w2] = h2.t;
+          if (world_hit<HAS_MESH, BVH, STATS>(S, r2, 0.001, INFINITY, h2, w2, stk, st) && z) A.out[w2] = h2.t;
         }
 #endif
-        if (!world_hit<HAS_MESH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
+        if (!world_hit<HAS_MESH, BVH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
           const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
           R = T * S.background[bin];
           term = true;
@@ -936,7 +1032,10 @@ __global__ __launch_bounds__(256) void k_intersect(DevScene S, const double* __r
   int32_t which = -1;
   Stats st;
   double* o = hits + 8 * (size_t)i;
-  if (world_hit<true, false>(S, r, q[6], q[7], h, which, &s_stack[wave * kStackSlots * 64 + lane], st)) {
+  uint32_t* stk = &s_stack[wave * kStackSlots * 64 + lane];
+  const bool hit = S.world_nodes ? world_hit<false, true, false>(S, r, q[6], q[7], h, which, stk, st)
+                                 : world_hit<true, false, false>(S, r, q[6], q[7], h, which, stk, st);
+  if (hit) {
     o[0] = h.t; o[1] = h.p.x; o[2] = h.p.y; o[3] = h.p.z;
     o[4] = h.n.x; o[5] = h.n.y; o[6] = h.n.z; o[7] = h.ff ? 1.0 : 0.0;
   } else {
@@ -1007,13 +1106,17 @@ hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hip
   if (grid == 0) return hipSuccess;
   const bool dyn = a.scratch != nullptr;  // stats launches are always fused (see capi.cpp)
   if (s.has_mesh) {
-    if (stats) hipLaunchKernelGGL((k_render<true, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
-    else if (dyn) hipLaunchKernelGGL((k_render<true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<true, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (stats) hipLaunchKernelGGL((k_render<true, false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<true, false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+  } else if (s.world_nodes) {
+    if (stats) hipLaunchKernelGGL((k_render<false, true, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<false, true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<false, true, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
   } else {
-    if (stats) hipLaunchKernelGGL((k_render<false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
-    else if (dyn) hipLaunchKernelGGL((k_render<false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (stats) hipLaunchKernelGGL((k_render<false, false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<false, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<false, false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
   }
   return hipGetLastError();
 }

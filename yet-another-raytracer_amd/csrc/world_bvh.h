@@ -1,0 +1,27 @@
+// world_bvh.h — host-side build of the world BVH (DevWorldNode) over a scene's object list.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "device_types.h"
+#include "../../include/yart.h"
+
+namespace yart_dev {
+
+struct BuiltWorld {
+  std::vector<DevWorldNode> nodes;  // root = nodes[0]
+  std::vector<uint32_t> objs;       // leaf slots -> object index
+  uint32_t depth = 0;               // inner levels on the deepest root-to-leaf path
+};
+
+// World-space bounds of one list entry: the primitive's own box (sphere ± |r|, rect extent with
+// its plane coordinate, box corners, triangle vertices) carried through its wrappers innermost
+// first as hit_record undoes them (RotateY's back rotation on the 8 corners, Translate's offset).
+// false for kinds that have no box here (meshes: those scenes keep the linear walk).
+bool world_bounds(const DevObject& o, double lo[3], double hi[3]);
+
+// Median split on the centroid's widest axis down to <= 2 objects per leaf; boxes are padded by
+// 1e-7 of their magnitude and rounded outward to f32. false if some object has no box.
+bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out);
+
+}  // namespace yart_dev

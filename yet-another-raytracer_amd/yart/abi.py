@@ -59,7 +59,8 @@ class RenderParams(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("device", C.c_int), ("n_objects", C.c_uint32), ("n_lights", C.c_uint32), ("n_meshes", C.c_uint32),
                 ("bvh_nodes", C.c_uint32), ("bvh_leaves", C.c_uint32), ("bvh_max_depth", C.c_uint32),
-                ("bvh_max_stack", C.c_uint32), ("device_bytes", C.c_uint64)]
+                ("bvh_max_stack", C.c_uint32), ("device_bytes", C.c_uint64), ("world_nodes", C.c_uint32),
+                ("world_depth", C.c_uint32)]
 
 
 class RenderStats(C.Structure):
