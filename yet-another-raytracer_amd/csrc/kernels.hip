@@ -775,7 +775,10 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 // no lane idles while another still has samples of its own pixel left. Safe because each
 // (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN>
-__global__ __launch_bounds__(256, HAS_MESH ? 2 : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
+#ifndef YART_MESH_WAVES_PER_EU
+#define YART_MESH_WAVES_PER_EU 4  // 128 VGPRs; traversal is latency-bound: +36% on david over 2
+#endif
+__global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[(HAS_MESH || BVH) ? 4 * kStackSlots * 64 : 1];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
@@ -1020,7 +1023,7 @@ __global__ __launch_bounds__(256) void k_accumulate(RenderArgs A, int first_pass
 }
 
 // ------------------------------------------------------------------- batched closest hit
-__global__ __launch_bounds__(256) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
+__global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
                                                    double* __restrict__ hits, int32_t* __restrict__ obj) {
   __shared__ uint32_t s_stack[4 * kStackSlots * 64];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
