@@ -293,6 +293,7 @@ static int make_args(const yart_scene* s, const yart_camera* cam, const yart_ren
   a.out = out;
   a.scratch = nullptr;
   a.stats = nullptr;
+  a.queue = nullptr; a.n_units = 0; a.waves = 0;
   return YART_OK;
 }
 
@@ -377,7 +378,9 @@ static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool st
     return YART_OK;
   }
   double* scratch = nullptr;
-  if (int rc = get_scratch(s, stream, (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double), &scratch)) return rc;
+  const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
+  if (int rc = get_scratch(s, stream, scratch_bytes + 256, &scratch)) return rc;  // + the unit counter
+  uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + scratch_bytes);
   const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
   if (int rc = timing_events(s, stream, 3 * (size_t)passes, &ev)) return rc;
   uint32_t k = 0;
@@ -388,6 +391,10 @@ static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool st
     b.chunk = pl.chunk;
     b.n_chunks = (b.s_count + pl.chunk - 1) / pl.chunk;
     b.scratch = scratch;
+    b.queue = queue;
+    b.n_units = b.n_blocks * b.n_chunks;
+    b.waves = (uint32_t)s->cu_count * 16;  // 4 waves per SIMD resident
+    HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream), "zero the unit counter");
     HIP_TRY(hipEventRecord((*ev)[3 * k], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
     HIP_TRY(hipEventRecord((*ev)[3 * k + 1], stream), "hipEventRecord");

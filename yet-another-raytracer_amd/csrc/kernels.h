@@ -18,6 +18,9 @@ struct RenderArgs {
   // Work units = n_blocks x n_chunks; unit u renders block u % n_blocks for samples
   // [s_begin + (u / n_blocks) * chunk, ... + chunk) clipped to [s_begin, s_begin + s_count).
   uint32_t s_begin, s_count, chunk, n_chunks;
+  uint32_t* queue;    // chunked path: unit counter (zeroed before each launch), claimed by persistent waves
+  uint32_t n_units;   // n_blocks * n_chunks
+  uint32_t waves;     // chunked path: resident waves to launch (CUs x 16)
   double* out;        // width * height * 3 (fused path: final sums; written by k_accumulate otherwise)
   double* scratch;    // null = fused; else n_blocks * s_count * 64 * 3 per-sample XYZ
   unsigned long long* stats;  // 8 counters (STATS build only)

@@ -784,11 +784,14 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
   // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
   // one XCD all the expensive glass-sphere blocks: 1,960 vs 2,507 Msamples/s measured.)
-  const uint32_t work = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-  if (work >= A.n_blocks * A.n_chunks) return;
-  const uint32_t local_blk = work % A.n_blocks, chunk_id = work / A.n_blocks;
-  const uint32_t b = A.shard_index + local_blk * A.shard_count;
-  const uint32_t bx0 = (b % A.blocks_x) * 8, by0 = (b / A.blocks_x) * 8;
+  // DYN: persistent waves — the grid is one resident wave per slot, and each wave claims units
+  // from A.queue (one atomic per unit) until they run out; the wave's lanes flow from one unit's
+  // jobs into the next, so no wave drains a unit's last long paths with idle lanes.
+  uint32_t work = DYN ? 0u : xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  if (!DYN && work >= A.n_blocks * A.n_chunks) return;
+  uint32_t local_blk = work % A.n_blocks, chunk_id = work / A.n_blocks;
+  uint32_t b = A.shard_index + local_blk * A.shard_count;
+  uint32_t bx0 = (b % A.blocks_x) * 8, by0 = (b / A.blocks_x) * 8;
   uint32_t slot = lane;  // pixel slot in the 8x8 block this lane is working on
   uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
@@ -800,15 +803,15 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   uint32_t pixel = y * W + x;
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   const uint32_t s_end = A.s_begin + A.s_count;
-  const uint32_t s_lo = A.s_begin + chunk_id * A.chunk;
+  uint32_t s_lo = A.s_begin + chunk_id * A.chunk;
   const uint32_t s_stop = s_lo + A.chunk < s_end ? s_lo + A.chunk : s_end;
   uint32_t smp = s_lo;
-  // scratch of this unit's block: [local_blk][sample - s_begin][slot][xyz]
-  double* const sblk = A.scratch ? A.scratch + 3 * (size_t)local_blk * A.s_count * 64 : nullptr;
-  const uint32_t n_jobs = (s_stop > s_lo ? s_stop - s_lo : 0) * 64;
-  uint32_t next_job = 0;  // wave-uniform (DYN)
-  bool need = true;       // DYN: this lane wants a job
-  bool alive = DYN ? (n_jobs > 0) : (active && smp < s_stop);
+  // scratch: [local_blk][sample - s_begin][slot][xyz]; DYN lanes keep their job's block
+  uint32_t lane_blk = local_blk;
+  uint32_t n_jobs = 0, next_job = 0;  // the wave's current unit (DYN, wave-uniform)
+  bool drained = false;               // DYN: the queue has no units left (wave-uniform)
+  bool need = true;                   // DYN: this lane wants a job
+  bool alive = DYN ? true : (active && smp < s_stop);
   Rng g;
   Ray ray;
   double T = 1.0;
@@ -820,24 +823,41 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
 
   while (alive) {
     if (DYN) {
-      const uint64_t m = __ballot(need);
-      if (need) {
+      uint64_t m = drained ? 0ull : __ballot(need);
+      while (m) {  // wave-uniform: hand out jobs until every asking lane has one
+        if (next_job >= n_jobs) {  // claim the next unit
+          const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
+          uint32_t v = 0;
+          if (lane == first) v = atomicAdd(A.queue, 1u);
+          const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)first);
+          if (u >= A.n_units) { drained = true; break; }
+          local_blk = u % A.n_blocks; chunk_id = u / A.n_blocks;
+          b = A.shard_index + local_blk * A.shard_count;
+          bx0 = (b % A.blocks_x) * 8; by0 = (b / A.blocks_x) * 8;
+          s_lo = A.s_begin + chunk_id * A.chunk;
+          const uint32_t stop = s_lo + A.chunk < s_end ? s_lo + A.chunk : s_end;
+          n_jobs = (stop > s_lo ? stop - s_lo : 0) * 64;
+          next_job = 0;
+          continue;
+        }
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint32_t job = next_job + rank;
-        if (job >= n_jobs) {
-          alive = false;
-        } else {
+        const uint32_t avail = n_jobs - next_job;
+        if (need && rank < avail) {
+          const uint32_t job = next_job + rank;
           slot = job & 63u;
           smp = s_lo + (job >> 6);
           x = bx0 + (slot & 7u);
           y = by0 + (slot >> 3);
           pixel = y * W + x;
+          lane_blk = local_blk;
+          // a pixel outside the crop grid is skipped: the lane asks again
           if (x < W && y < H && covered(x, W) && covered(y, H)) { fresh = true; need = false; }
         }
+        const uint32_t given = (uint32_t)__popcll(m);
+        next_job += given < avail ? given : avail;
+        m = __ballot(need);
       }
-      next_job += (uint32_t)__popcll(m);
-      if (!alive) break;
-      if (need) continue;  // the job's pixel is outside the crop grid: take another
+      if (need) break;  // the queue is drained: no job for this lane
     }
     // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
     // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
@@ -980,7 +1000,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
       if (STATS) st.v[ST_SAMPLES]++;
       if (DYN) {  // chunked: k_accumulate adds the samples in order
-        double* q = sblk + 3 * ((size_t)(smp - A.s_begin) * 64 + slot);
+        double* q = A.scratch + 3 * (((size_t)lane_blk * A.s_count + (smp - A.s_begin)) * 64 + slot);
         q[0] = sx; q[1] = sy; q[2] = sz;
         need = true;
       } else {
@@ -1105,9 +1125,10 @@ hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t s
   return hipGetLastError();
 }
 hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream) {
-  const uint32_t grid = (a.n_blocks * a.n_chunks + 3) / 4;
-  if (grid == 0) return hipSuccess;
   const bool dyn = a.scratch != nullptr;  // stats launches are always fused (see capi.cpp)
+  const uint32_t units = a.n_blocks * a.n_chunks;
+  const uint32_t grid = ((dyn && a.waves < units ? a.waves : units) + 3) / 4;
+  if (grid == 0) return hipSuccess;
   if (s.has_mesh) {
     if (stats) hipLaunchKernelGGL((k_render<true, false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
     else if (dyn) hipLaunchKernelGGL((k_render<true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
