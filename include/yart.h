@@ -43,14 +43,32 @@ typedef enum yart_status {
 
 /* ---------------------------------------------------------------- textures (texture.rs) */
 enum {
-  YART_TEX_SOLID = 0,  /* SolidColor<RGB>            texture.rs:18-40 */
-  YART_TEX_CHECKER = 1 /* CheckerTexture<RGB>        texture.rs:42-68 */
+  YART_TEX_SOLID = 0,   /* SolidColor<RGB>            texture.rs:18-40   */
+  YART_TEX_CHECKER = 1, /* CheckerTexture<RGB>        texture.rs:42-68   */
+  YART_TEX_NOISE = 2    /* NoiseTexture (Perlin)      texture.rs:262-300 */
 };
+enum { /* NoiseType, texture.rs:70-82 */
+  YART_NOISE_SQUARE = 0,
+  YART_NOISE_TRILINEAR = 1,
+  YART_NOISE_SMOOTH = 2,
+  YART_NOISE_MARBLE = 3,
+  YART_NOISE_NET = 4
+};
+/* Perlin tables (texture.rs:84-112, POINT_COUNT = 256), drawn by the scene builder. */
+typedef struct yart_perlin {
+  double ranfloat[256];
+  double ranvec[256][3];
+  int32_t perm_x[256];
+  int32_t perm_y[256];
+  int32_t perm_z[256];
+} yart_perlin;
 typedef struct yart_texture {
   uint32_t kind;
-  uint32_t reserved;
-  double rgb[3];      /* SOLID: the colour.  CHECKER: the `odd` colour (sines < 0). */
-  double rgb_even[3]; /* CHECKER: the `even` colour.                                */
+  uint32_t noise_type;       /* NOISE: YART_NOISE_*                                       */
+  double rgb[3];             /* SOLID: the colour.  CHECKER: the `odd` colour (sines < 0). */
+  double rgb_even[3];        /* CHECKER: the `even` colour.                                */
+  double scale;              /* NOISE: NoiseTexture::scale                                 */
+  const yart_perlin* perlin; /* NOISE: its tables (copied by yart_scene_create)            */
 } yart_texture;
 
 /* --------------------------------------------------------------- materials (material.rs) */
@@ -59,7 +77,8 @@ enum {
   YART_MAT_LAMBERTIAN = 1,    /* Lambertian<T>       material.rs:33-61   */
   YART_MAT_METAL = 2,         /* Metal<T>            material.rs:63-95   */
   YART_MAT_DIELECTRIC = 3,    /* Dielectric          material.rs:111-301 (Sellmeier b, c in nm^2) */
-  YART_MAT_DIFFUSE_LIGHT = 4  /* DiffuseLight<T>     material.rs:336-355 */
+  YART_MAT_DIFFUSE_LIGHT = 4, /* DiffuseLight<T>     material.rs:336-355 */
+  YART_MAT_ISOTROPIC = 5      /* Isotropic<T>        material.rs:357-381 (phase function of a medium) */
 };
 typedef struct yart_material {
   uint32_t kind;
@@ -82,7 +101,10 @@ enum {
 enum {
   YART_XF_TRANSLATE = 1, /* Translate  hittable.rs:125-163  v = offset            */
   YART_XF_ROTATE_Y = 2,  /* RotateY    hittable.rs:165-256  v[0] = angle, degrees */
-  YART_XF_FLIP_FACE = 3  /* FlipFace   hittable.rs:328-354                        */
+  YART_XF_FLIP_FACE = 3, /* FlipFace   hittable.rs:328-354                        */
+  YART_XF_MEDIUM = 4     /* ConstantMedium hittable.rs:258-326, v[0] = density; only as the
+                            OUTERMOST wrapper: the rest of the chain + the primitive is its
+                            boundary, the object's material its phase function (Isotropic) */
 };
 typedef struct yart_xform {
   uint32_t kind;

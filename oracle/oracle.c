@@ -121,12 +121,73 @@ double oracle_cos(double x) {
   }
 }
 
+/* Deterministic natural log shared bit for bit with the device (libm's log differs between glibc
+ * and ROCm's ocml in the last ulp): fdlibm's __ieee754_log (Sun, 1993) — reduction to
+ * f in [sqrt(2)/2 - 1, sqrt(2) - 1), s = f / (2 + f), and the Lg1..Lg7 minimax polynomial in s^2.
+ * Only + - * / and exponent bit arithmetic. Used by ConstantMedium (hittable.rs:303). */
+double oracle_log(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+               Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+  uint64_t bits; memcpy(&bits, &x, 8);
+  int32_t hx = (int32_t)(bits >> 32);
+  uint32_t lx = (uint32_t)bits;
+  int k = 0;
+  if (hx < 0x00100000) {                              /* x < 2^-1022 */
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -INFINITY; /* log(+-0) */
+    if (hx < 0) return NAN;                          /* log(-#) */
+    k -= 54; x *= two54;                             /* subnormal: scale up */
+    memcpy(&bits, &x, 8); hx = (int32_t)(bits >> 32);
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000;
+  memcpy(&bits, &x, 8);
+  bits = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (bits & 0xffffffffu); /* x or x/2 in [sqrt2/2, sqrt2) */
+  memcpy(&x, &bits, 8);
+  k += (i >> 20);
+  double f = x - 1.0, dk, R;
+  if ((0x000fffff & (2 + hx)) < 3) {                 /* |f| < 2^-20 */
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      dk = (double)k;
+      return dk * ln2_hi + dk * ln2_lo;
+    }
+    R = f * f * (0.5 - 0.33333333333333333 * f);
+    if (k == 0) return f - R;
+    dk = (double)k;
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  double s = f / (2.0 + f);
+  dk = (double)k;
+  double z = s * s;
+  i = hx - 0x6147a;
+  double w = z * z;
+  int32_t j = 0x6b851 - hx;
+  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  i |= j;
+  R = t2 + t1;
+  if (i > 0) {
+    double hfsq = 0.5 * f * f;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  if (k == 0) return f - s * (f - R);
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
 /* f64::powi(x, 5) as LLVM expands it: x * ((x*x) * (x*x)) (material.rs:210). */
 static inline double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }
 
 /* ------------------------------------------------------------------------ RNG
  * Philox4x32-10 (Salmon et al., SC'11; Random123) keyed by the 64-bit seed, counter
- * (block, sample, pixel, phase << 1 | stream). Each block yields two u64 draws, taken in order.
+ * (block, sample, pixel, phase << 2 | stream). Each block yields two u64 draws, taken in order.
+ * Streams: 0 the path's draws, 1 scene construction (host SceneRng), 2 ConstantMedium's
+ * free-path draw — keyed (object index, sample, pixel, segment), one per medium per world query,
+ * so it does not depend on the order the objects are visited in.
  * A path's draws are split into phases, each with its own run of blocks from block 0: phase 0
  * is the camera ray (main.rs:692-698), phase k >= 1 the scatter at the k-th bounce
  * (max_depth - depth + 1 of ray_reflectance main.rs:537). The reference draws from
@@ -154,7 +215,7 @@ static void rng_init(rng_t* r, uint64_t seed, uint32_t pixel, uint32_t sample, u
   r->have = 0;
 }
 static void rng_phase(rng_t* r, uint32_t phase) {
-  r->ctr[0] = 0; r->ctr[3] = (phase << 1) | (r->ctr[3] & 1u);
+  r->ctr[0] = 0; r->ctr[3] = (phase << 2) | (r->ctr[3] & 3u);
   r->have = 0;
 }
 static inline uint64_t rng_u64(rng_t* r) {
@@ -187,6 +248,14 @@ static inline uint64_t gen_range_usize(rng_t* r, uint64_t n) {
     uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
     if (lo <= zone) return hi;
   }
+}
+
+/* ConstantMedium's rng.gen::<f64>() (hittable.rs:303) for object `obj` at world query `seg`. */
+static double medium_draw(uint64_t seed, uint32_t obj, uint32_t sample, uint32_t pixel, uint32_t seg) {
+  const uint32_t ctr[4] = {obj, sample, pixel, (seg << 2) | 2u}, key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t out[4];
+  oracle_philox4x32_10(ctr, key, out);
+  return (double)((((uint64_t)out[1] << 32) | out[0]) >> 11) * 0x1.0p-53;
 }
 
 void oracle_rng_f64(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, double* out) {
@@ -304,6 +373,7 @@ struct oracle_scene {
   yart_object* lights; uint32_t nlights;
   yart_material* mats; uint32_t nmats;
   yart_texture* texs; uint32_t ntexs;
+  yart_perlin* perlins; /* per texture (NOISE) */
   qbvh_t* meshes; uint32_t nmeshes;
   double background[3];
   /* per object, per wrapper: RotateY sin/cos (hittable.rs:173-176) */
@@ -623,14 +693,36 @@ static int prim_hit(const oracle_scene* s, const yart_object* o, const ray_t* r,
 }
 
 /* Wrappers, outermost first: Translate (hittable.rs:136-152), RotateY (:217-251), FlipFace (:338-349). */
+/* Where a world query happens: keys ConstantMedium's draw (stream 2, see the RNG notes). */
+typedef struct { uint64_t seed; uint32_t sample, pixel, seg; } wctx_t;
+
 static int object_hit(const oracle_scene* s, const yart_object* o, const double (*sc)[2], uint32_t level,
-                      const ray_t* r, double t_min, double t_max, hit_rec* rec) {
+                      const ray_t* r, double t_min, double t_max, hit_rec* rec, const wctx_t* cx, uint32_t obj) {
   if (level == o->n_xforms) return prim_hit(s, o, r, t_min, t_max, rec);
   const yart_xform* x = &o->xforms[level];
+  if (x->kind == YART_XF_MEDIUM) { /* ConstantMedium::hit hittable.rs:277-318 */
+    hit_rec rec1, rec2;
+    if (!object_hit(s, o, sc, level + 1, r, -INFINITY, INFINITY, &rec1, cx, obj)) return 0;
+    if (!object_hit(s, o, sc, level + 1, r, rec1.t + 0.0001, INFINITY, &rec2, cx, obj)) return 0;
+    if (rec1.t < t_min) rec1.t = t_min;
+    if (rec2.t > t_max) rec2.t = t_max;
+    if (!(rec1.t < rec2.t)) return 0;
+    if (rec1.t < 0.0) rec1.t = 0.0;
+    const double ray_length = length(r->d);
+    const double distance_inside_boundary = (rec2.t - rec1.t) * ray_length;
+    const double neg_inv_density = -1.0 / x->v[0];
+    const double hit_distance = neg_inv_density * oracle_log(medium_draw(cx->seed, obj, cx->sample, cx->pixel, cx->seg));
+    if (!(hit_distance < distance_inside_boundary)) return 0;
+    rec->t = rec1.t + hit_distance / ray_length;
+    rec->p = ray_at(r, rec->t);
+    rec->normal = V(1.0, 0.0, 0.0);
+    rec->front_face = 1;
+    return 1;
+  }
   if (x->kind == YART_XF_TRANSLATE) {
     v3 off = V(x->v[0], x->v[1], x->v[2]);
     ray_t moved = {vsub(r->o, off), r->d, r->time, r->wl};
-    if (!object_hit(s, o, sc, level + 1, &moved, t_min, t_max, rec)) return 0;
+    if (!object_hit(s, o, sc, level + 1, &moved, t_min, t_max, rec, cx, obj)) return 0;
     rec->p = vadd(rec->p, off);
     return 1;
   }
@@ -641,7 +733,7 @@ static int object_hit(const oracle_scene* s, const yart_object* o, const double 
     rot.o.z = sn * r->o.x + cs * r->o.z;
     rot.d.x = cs * r->d.x - sn * r->d.z;
     rot.d.z = sn * r->d.x + cs * r->d.z;
-    if (!object_hit(s, o, sc, level + 1, &rot, t_min, t_max, rec)) return 0;
+    if (!object_hit(s, o, sc, level + 1, &rot, t_min, t_max, rec, cx, obj)) return 0;
     v3 p = rec->p, n = rec->normal;
     rec->p.x = cs * p.x + sn * p.z;
     rec->p.z = -sn * p.x + cs * p.z;
@@ -650,15 +742,16 @@ static int object_hit(const oracle_scene* s, const yart_object* o, const double 
     return 1;
   }
   /* FLIP_FACE */
-  if (!object_hit(s, o, sc, level + 1, r, t_min, t_max, rec)) return 0;
+  if (!object_hit(s, o, sc, level + 1, r, t_min, t_max, rec, cx, obj)) return 0;
   rec->front_face = !rec->front_face;
   return 1;
 }
 
-static int world_hit(const oracle_scene* s, const ray_t* r, double t_min, double t_max, hit_rec* rec, int32_t* which) { /* hittable.rs:67-79 */
+static int world_hit(const oracle_scene* s, const ray_t* r, double t_min, double t_max, hit_rec* rec, int32_t* which,
+                     const wctx_t* cx) { /* hittable.rs:67-79 */
   int found = 0; double closest = t_max; hit_rec tmp;
   for (uint32_t i = 0; i < s->nobj; ++i) {
-    if (object_hit(s, &s->objects[i], (const double (*)[2])s->obj_sc[i], 0, r, t_min, closest, &tmp)) {
+    if (object_hit(s, &s->objects[i], (const double (*)[2])s->obj_sc[i], 0, r, t_min, closest, &tmp, cx, i)) {
       closest = tmp.t;
       tmp.mat = s->objects[i].material;
       *rec = tmp; found = 1;
@@ -754,8 +847,68 @@ static v3 lights_random(const oracle_scene* s, v3 origin, rng_t* g) { /* hittabl
 }
 
 /* ------------------------------------------------------------------ textures / materials */
+/* Rust `f as i32`: saturating, NaN -> 0. */
+static int32_t sat_i32(double f) {
+  if (f != f) return 0;
+  if (f >= 2147483647.0) return INT32_MAX;
+  if (f <= -2147483648.0) return INT32_MIN;
+  return (int32_t)f;
+}
+/* Perlin::noise (texture.rs:114-180) */
+static double perlin_noise(const yart_perlin* P, uint32_t type, v3 p) {
+  if (type == YART_NOISE_SQUARE) {
+    const int32_t i = sat_i32(4.0 * p.x) & 255, j = sat_i32(4.0 * p.y) & 255, k = sat_i32(4.0 * p.z) & 255;
+    return P->ranfloat[P->perm_x[i] ^ P->perm_y[j] ^ P->perm_z[k]];
+  }
+  double u = p.x - floor(p.x), v = p.y - floor(p.y), w = p.z - floor(p.z);
+  const int32_t i = sat_i32(floor(p.x)), j = sat_i32(floor(p.y)), k = sat_i32(floor(p.z));
+  double accum = 0.0;
+  if (type == YART_NOISE_TRILINEAR) {
+    u = u * u * (3.0 - 2.0 * u);
+    v = v * v * (3.0 - 2.0 * v);
+    w = w * w * (3.0 - 2.0 * w);
+    for (int di = 0; di < 2; ++di)
+      for (int dj = 0; dj < 2; ++dj)
+        for (int dk = 0; dk < 2; ++dk) { /* trilinear_interp texture.rs:192-207 */
+          const double c = P->ranfloat[P->perm_x[((uint32_t)i + (uint32_t)di) & 255u] ^ P->perm_y[((uint32_t)j + (uint32_t)dj) & 255u] ^
+                                       P->perm_z[((uint32_t)k + (uint32_t)dk) & 255u]];
+          accum += ((double)di * u + (double)(1 - di) * (1.0 - u)) * ((double)dj * v + (double)(1 - dj) * (1.0 - v)) *
+                   ((double)dk * w + (double)(1 - dk) * (1.0 - w)) * c;
+        }
+    return accum;
+  }
+  const double uu = u * u * (3.0 - 2.0 * u), vv = v * v * (3.0 - 2.0 * v), ww = w * w * (3.0 - 2.0 * w);
+  for (int di = 0; di < 2; ++di)
+    for (int dj = 0; dj < 2; ++dj)
+      for (int dk = 0; dk < 2; ++dk) { /* perlin_interp texture.rs:209-228 */
+        const double* c = P->ranvec[P->perm_x[((uint32_t)i + (uint32_t)di) & 255u] ^ P->perm_y[((uint32_t)j + (uint32_t)dj) & 255u] ^
+                                    P->perm_z[((uint32_t)k + (uint32_t)dk) & 255u]];
+        const v3 weight_v = V(u - (double)di, v - (double)dj, w - (double)dk);
+        accum += ((double)di * uu + (1.0 - (double)di) * (1.0 - uu)) * ((double)dj * vv + (1.0 - (double)dj) * (1.0 - vv)) *
+                 ((double)dk * ww + (1.0 - (double)dk) * (1.0 - ww)) * dot(weight_v, V(c[0], c[1], c[2]));
+      }
+  return accum;
+}
+static double perlin_turb(const yart_perlin* P, uint32_t type, v3 p, int depth) { /* texture.rs:230-242 */
+  double accum = 0.0, weight = 1.0;
+  v3 temp_p = p;
+  for (int d = 0; d < depth; ++d) {
+    accum += weight * perlin_noise(P, type, temp_p);
+    weight *= 0.5;
+    temp_p = vmuls(temp_p, 2.0);
+  }
+  return fabs(accum);
+}
+
 static double texture_value(const oracle_scene* s, uint32_t ti, const ray_t* r, const hit_rec* rec) {
   const yart_texture* t = &s->texs[ti];
+  if (t->kind == YART_TEX_NOISE) { /* NoiseTexture::value texture.rs:265-300 (rgb = white) */
+    const double white = oracle_rgb_reflect(t->rgb, r->wl);
+    if (t->noise_type == YART_NOISE_NET) return white * perlin_turb(t->perlin, t->noise_type, vmuls(rec->p, t->scale), 7);
+    if (t->noise_type == YART_NOISE_MARBLE)
+      return white * 0.5 * (1.0 + oracle_sin(t->scale * rec->p.z + 10.0 * perlin_turb(t->perlin, t->noise_type, rec->p, 7)));
+    return white * 0.5 * (1.0 + perlin_noise(t->perlin, t->noise_type, vmuls(rec->p, t->scale)));
+  }
   if (t->kind == YART_TEX_CHECKER) { /* texture.rs:58-67 */
     double sines = oracle_sin(10.0 * rec->p.x) * oracle_sin(10.0 * rec->p.y) * oracle_sin(10.0 * rec->p.z);
     return sines < 0.0 ? oracle_rgb_reflect(t->rgb, r->wl) : oracle_rgb_reflect(t->rgb_even, r->wl);
@@ -818,7 +971,8 @@ static void bounce(const oracle_scene* s, const ray_t* r, rng_t* g, uint32_t pha
   hit_rec rec;
   rng_phase(g, phase);
   b->cont = 0;
-  if (!world_hit(s, r, 0.001, INFINITY, &rec, NULL)) {
+  const wctx_t cx = {((uint64_t)g->key[1] << 32) | g->key[0], g->ctr[1], g->ctr[2], phase};
+  if (!world_hit(s, r, 0.001, INFINITY, &rec, NULL, &cx)) {
     b->terminal = oracle_rgb_reflect(s->background, r->wl); /* main.rs:587 */
     return;
   }
@@ -854,6 +1008,13 @@ static void bounce(const oracle_scene* s, const ray_t* r, rng_t* g, uint32_t pha
       double att = texture_value(s, m->texture, r, &rec);
       b->cont = 1; b->kind = 0; b->att = att;
       b->next.o = rec.p; b->next.d = vadd(reflected, fz); b->next.time = r->time; b->next.wl = r->wl;
+      return;
+    }
+    case YART_MAT_ISOTROPIC: { /* material.rs:370-381: attenuation, then a random_in_unit_sphere direction */
+      double att = texture_value(s, m->texture, r, &rec);
+      v3 dir = random_in_unit_sphere(g);
+      b->cont = 1; b->kind = 0; b->att = att;
+      b->next.o = rec.p; b->next.d = dir; b->next.time = r->time; b->next.wl = r->wl;
       return;
     }
     case YART_MAT_DIELECTRIC: { /* material.rs:213-301 */
@@ -1021,13 +1182,22 @@ int oracle_finalize_rgba8(const double* xyz_sum, uint32_t w, uint32_t h, uint32_
   return YART_OK;
 }
 
+double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3]) {
+  ray_t r = {V(0.0, 0.0, 0.0), V(1.0, 0.0, 0.0), 0.0, wl};
+  hit_rec rec;
+  memset(&rec, 0, sizeof rec);
+  rec.p = V(p[0], p[1], p[2]);
+  return texture_value(s, tex, &r, &rec);
+}
+
 int oracle_intersect(const oracle_scene* s, const double* rays, uint32_t n, double* hits, int32_t* obj) {
   for (uint32_t i = 0; i < n; ++i) {
     const double* q = &rays[8 * (size_t)i];
     ray_t r = {V(q[0], q[1], q[2]), V(q[3], q[4], q[5]), 0.0, 0.0};
     hit_rec rec; int32_t which = -1;
     double* h = &hits[8 * (size_t)i];
-    if (world_hit(s, &r, q[6], q[7], &rec, &which)) {
+    const wctx_t cx = {0, 0, i, 0};  /* a medium's draw for query i: seed 0, sample 0, pixel i */
+    if (world_hit(s, &r, q[6], q[7], &rec, &which, &cx)) {
       h[0] = rec.t; h[1] = rec.p.x; h[2] = rec.p.y; h[3] = rec.p.z;
       h[4] = rec.normal.x; h[5] = rec.normal.y; h[6] = rec.normal.z; h[7] = rec.front_face ? 1.0 : 0.0;
     } else {
@@ -1057,7 +1227,9 @@ static int check_objects(const yart_scene_desc* d, const yart_object* o, uint32_
     if (o[i].kind == YART_PRIM_MESH && o[i].mesh >= d->n_meshes) return 0;
     if (o[i].material >= d->n_materials && d->n_materials) return 0;
     for (uint32_t l = 0; l < o[i].n_xforms; ++l)
-      if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_FLIP_FACE) return 0;
+      if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_MEDIUM ||
+          (o[i].xforms[l].kind == YART_XF_MEDIUM && l != 0))
+        return 0;
   }
   return 1;
 }
@@ -1066,9 +1238,14 @@ int oracle_scene_create(const yart_scene_desc* d, oracle_scene** out) {
   if (!d || !out || d->abi_version != YART_ABI_VERSION) return YART_ERR_INVALID;
   if (!check_objects(d, d->objects, d->n_objects) || !check_objects(d, d->lights, d->n_lights)) return YART_ERR_INVALID;
   for (uint32_t i = 0; i < d->n_materials; ++i)
-    if (d->materials[i].kind > YART_MAT_DIFFUSE_LIGHT ||
+    if (d->materials[i].kind > YART_MAT_ISOTROPIC ||
         ((d->materials[i].kind == YART_MAT_LAMBERTIAN || d->materials[i].kind == YART_MAT_METAL ||
-          d->materials[i].kind == YART_MAT_DIFFUSE_LIGHT) && d->materials[i].texture >= d->n_textures))
+          d->materials[i].kind == YART_MAT_DIFFUSE_LIGHT || d->materials[i].kind == YART_MAT_ISOTROPIC) &&
+         d->materials[i].texture >= d->n_textures))
+      return YART_ERR_INVALID;
+  for (uint32_t i = 0; i < d->n_textures; ++i)
+    if (d->textures[i].kind > YART_TEX_NOISE ||
+        (d->textures[i].kind == YART_TEX_NOISE && (!d->textures[i].perlin || d->textures[i].noise_type > YART_NOISE_NET)))
       return YART_ERR_INVALID;
   for (uint32_t i = 0; i < d->n_objects; ++i)
     if (d->objects[i].material >= d->n_materials) return YART_ERR_INVALID;
@@ -1082,6 +1259,9 @@ int oracle_scene_create(const yart_scene_desc* d, oracle_scene** out) {
   if (s->nlights) memcpy(s->lights, d->lights, sizeof(yart_object) * s->nlights);
   if (s->nmats) memcpy(s->mats, d->materials, sizeof(yart_material) * s->nmats);
   if (s->ntexs) memcpy(s->texs, d->textures, sizeof(yart_texture) * s->ntexs);
+  s->perlins = (yart_perlin*)calloc(s->ntexs + 1, sizeof(yart_perlin)); /* own copies of the tables */
+  for (uint32_t i = 0; i < s->ntexs; ++i)
+    if (s->texs[i].kind == YART_TEX_NOISE) { s->perlins[i] = *d->textures[i].perlin; s->texs[i].perlin = &s->perlins[i]; }
   memcpy(s->background, d->background, sizeof(s->background));
   s->obj_sc = calloc(s->nobj + 1, sizeof(*s->obj_sc));
   s->light_sc = calloc(s->nlights + 1, sizeof(*s->light_sc));
@@ -1102,7 +1282,7 @@ void oracle_scene_destroy(oracle_scene* s) {
     qbvh_t* q = &s->meshes[m];
     free(q->vert); free(q->norm); free(q->nodes); free(q->leaves); free(q->leaf_of_first);
   }
-  free(s->meshes); free(s->objects); free(s->lights); free(s->mats); free(s->texs);
+  free(s->meshes); free(s->objects); free(s->lights); free(s->mats); free(s->texs); free(s->perlins);
   free(s->obj_sc); free(s->light_sc);
   free(s);
 }

@@ -66,6 +66,9 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 double oracle_gen_range_f64(uint64_t seed, uint32_t pixel, uint32_t sample, double lo, double hi);
 double oracle_sin(double x); /* deterministic sin/cos shared bit-for-bit with the device */
 double oracle_cos(double x);
+double oracle_log(double x); /* deterministic natural log (fdlibm), shared bit-for-bit with the device */
+/* Texture::value of texture `tex` at point p and wavelength wl (known-answer tests). */
+double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3]);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,9 @@ CASES = [
     ("random_scene_36x24x4", "random-scene", 36, 24, 4, 50),
     ("bunny_standin_24x24x2", "bunny", 24, 24, 2, 50),
     ("david_32x18x2", "david", 32, 18, 2, 50),
+    ("two_perlin_spheres_40x24x4", "two-perlin-spheres", 40, 24, 4, 50),  # Perlin marble
+    ("simple_light_40x24x4", "simple-light", 40, 24, 4, 50),
+    ("cornell_smoke_32x32x4", "cornell-box-smoke", 32, 32, 4, 50),  # ConstantMedium + Isotropic
 ]
 
 

@@ -43,6 +43,8 @@ def lib():
         "oracle_gen_range_f64": (D, [U64, U32, U32, D, D]),
         "oracle_sin": (D, [D]),
         "oracle_cos": (D, [D]),
+        "oracle_log": (D, [D]),
+        "oracle_texture_probe": (D, [P, U32, D, P]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -78,6 +80,10 @@ class OracleScene:
         rc = lib().oracle_render(self._s, C.byref(cam), C.byref(params), _p(out), threads, 1 if recursive else 0)
         assert rc == 0
         return out
+
+    def texture(self, tex, wl, p):
+        pt = np.ascontiguousarray(p, dtype=np.float64)
+        return lib().oracle_texture_probe(self._s, tex, wl, _p(pt))
 
     def intersect(self, rays):
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
@@ -122,6 +128,27 @@ class DescBuilder:
         t.rgb = (C.c_double * 3)(*rgb)
         if rgb_even is not None:
             t.rgb_even = (C.c_double * 3)(*rgb_even)
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def noise_texture(self, noise_type, scale, seed=7):
+        """A NoiseTexture with Perlin tables drawn from numpy (any tables are valid input)."""
+        rng = np.random.default_rng(seed)
+        P = abi.Perlin()
+        for i, v in enumerate(rng.uniform(0, 1, 256)):
+            P.ranfloat[i] = v
+        for i, v in enumerate(rng.uniform(-1, 1, (256, 3))):
+            for k in range(3):
+                P.ranvec[i][k] = v[k]
+        for name in ("perm_x", "perm_y", "perm_z"):
+            arr = getattr(P, name)
+            for i, v in enumerate(rng.permutation(256)):
+                arr[i] = int(v)
+        self._keep.append(P)
+        t = abi.Texture()
+        t.kind, t.noise_type, t.scale = abi.TEX_NOISE, noise_type, scale
+        t.rgb = (C.c_double * 3)(1.0, 1.0, 1.0)
+        t.perlin = C.pointer(P)
         self.textures.append(t)
         return len(self.textures) - 1
 

@@ -59,6 +59,13 @@ def test_device_sin_cos_match_oracle(dev):
     np.testing.assert_array_equal(_probe(dev, 3, a), np.array([L.oracle_cos(x) for x in a]))
 
 
+def test_device_log_matches_oracle(dev):
+    rng = np.random.default_rng(6)
+    a = np.concatenate([rng.uniform(0, 1, 50000), 10.0 ** rng.uniform(-300, 300, 20000), [0.0, 1.0, 5e-324]])
+    L = O.lib()
+    np.testing.assert_array_equal(_probe(dev, 5, a), np.array([L.oracle_log(x) for x in a]))
+
+
 def _hits_equal(h1, o1, h2, o2):
     np.testing.assert_array_equal(o1, o2)
     m = o1 >= 0
@@ -86,11 +93,12 @@ def _random_rays(n, lo, hi, seed):
     return r
 
 
-@pytest.mark.parametrize("scene", ["cornell-box", "david", "sycee", "three-spheres", "random-scene"])
+@pytest.mark.parametrize("scene", ["cornell-box", "david", "sycee", "three-spheres", "random-scene", "cornell-box-smoke",
+                                   "two-perlin-spheres"])
 def test_intersect_matches_oracle(dev, scene):
     p = yart.Preset(scene)
     bounds = {"cornell-box": (0, 555), "david": (-150, 250), "sycee": (-4, 4), "three-spheres": (-3, 3),
-              "random-scene": (-12, 12)}[scene]
+              "random-scene": (-12, 12), "cornell-box-smoke": (0, 555), "two-perlin-spheres": (-6, 6)}[scene]
     rays = _random_rays(200000, *bounds, seed=11)
     # camera-like rays too: from the preset's eye towards the scene
     eye = np.array(p.defaults.lookfrom)
@@ -203,6 +211,9 @@ RENDER_CASES = [
     ("bunny", 40, 40, 4, 50),           # C4 (stand-in mesh) at reduced size
     ("david", 48, 27, 2, 50),           # C5 at reduced size (2 mesh instances)
     ("cornell-box", 16, 16, 3, 1),      # depth 1: every path ends at `depth == 0 -> 1.0`
+    ("two-perlin-spheres", 40, 24, 4, 50),  # NoiseTexture (Perlin marble), no lights
+    ("simple-light", 40, 24, 32, 50),       # + an XY-rect emitter (dark: more samples)
+    ("cornell-box-smoke", 32, 32, 4, 50),   # ConstantMedium + Isotropic (free-path draws, stream 2)
 ]
 
 
@@ -221,7 +232,7 @@ def test_render_bitwise_equal_to_oracle(dev, scene, W, H, spp, depth):
 
 
 @pytest.mark.parametrize("scene,spu", [("cornell-box", 1), ("cornell-box", 3), ("cornell-box", 7), ("david", 2),
-                                       ("random-scene", 5)])
+                                       ("random-scene", 5), ("cornell-box-smoke", 3)])
 def test_chunked_samples_bitwise_equal_to_sequential_sum(dev, scene, spu):
     """samples_per_unit < spp: per-sample values go through HBM and k_accumulate adds them in
     sample order; the sums must not change (main.rs:707's sequential +=)."""

@@ -87,8 +87,14 @@ bool valid_objects(const yart_scene_desc* d, const yart_object* o, uint32_t n, b
   for (uint32_t i = 0; i < n; ++i) {
     if (o[i].kind > YART_PRIM_MESH) { why = "object kind out of range"; return false; }
     if (o[i].n_xforms > YART_MAX_XFORMS) { why = "too many wrappers"; return false; }
-    for (uint32_t l = 0; l < o[i].n_xforms; ++l)
-      if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_FLIP_FACE) { why = "bad wrapper kind"; return false; }
+    for (uint32_t l = 0; l < o[i].n_xforms; ++l) {
+      if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_MEDIUM) { why = "bad wrapper kind"; return false; }
+      if (o[i].xforms[l].kind == YART_XF_MEDIUM && l != 0) { why = "a medium must be the outermost wrapper"; return false; }
+    }
+    if (o[i].n_xforms && o[i].xforms[0].kind == YART_XF_MEDIUM && o[i].kind == YART_PRIM_MESH) {
+      why = "a mesh as a medium boundary";
+      return false;
+    }
     if (o[i].kind == YART_PRIM_MESH && o[i].mesh >= d->n_meshes) { why = "mesh index out of range"; return false; }
     if (!lights && o[i].material >= d->n_materials) { why = "material index out of range"; return false; }
   }
@@ -104,6 +110,8 @@ DevObject to_dev(const yart_object& o) {
       const double radians = o.xforms[l].v[0] * 3.141592653589793 / 180.0;
       d.xf[l][0] = std::sin(radians);
       d.xf[l][1] = std::cos(radians);
+    } else if (o.xforms[l].kind == YART_XF_MEDIUM) {  // ConstantMedium::new (hittable.rs:270)
+      d.xf[l][0] = -1.0 / o.xforms[l].v[0];
     } else {
       for (int k = 0; k < 3; ++k) d.xf[l][k] = o.xforms[l].v[k];
     }
@@ -168,12 +176,16 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     return fail(YART_ERR_INVALID, why);
   for (uint32_t i = 0; i < d->n_materials; ++i) {
     const yart_material& m = d->materials[i];
-    if (m.kind > YART_MAT_DIFFUSE_LIGHT) return fail(YART_ERR_INVALID, "material kind out of range");
-    bool textured = m.kind == YART_MAT_LAMBERTIAN || m.kind == YART_MAT_METAL || m.kind == YART_MAT_DIFFUSE_LIGHT;
+    if (m.kind > YART_MAT_ISOTROPIC) return fail(YART_ERR_INVALID, "material kind out of range");
+    bool textured = m.kind == YART_MAT_LAMBERTIAN || m.kind == YART_MAT_METAL || m.kind == YART_MAT_DIFFUSE_LIGHT ||
+                    m.kind == YART_MAT_ISOTROPIC;
     if (textured && m.texture >= d->n_textures) return fail(YART_ERR_INVALID, "texture index out of range");
   }
-  for (uint32_t i = 0; i < d->n_textures; ++i)
-    if (d->textures[i].kind > YART_TEX_CHECKER) return fail(YART_ERR_INVALID, "texture kind out of range");
+  for (uint32_t i = 0; i < d->n_textures; ++i) {
+    if (d->textures[i].kind > YART_TEX_NOISE) return fail(YART_ERR_INVALID, "texture kind out of range");
+    if (d->textures[i].kind == YART_TEX_NOISE && (!d->textures[i].perlin || d->textures[i].noise_type > YART_NOISE_NET))
+      return fail(YART_ERR_INVALID, "noise texture without Perlin tables or with a bad noise type");
+  }
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
   if (device < 0 || device >= ndev) return fail(YART_ERR_INVALID, "device index out of range");
@@ -192,6 +204,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   for (uint32_t i = 0; i < d->n_textures; ++i) {
     const yart_texture& t = d->textures[i];
     texs[i].kind = t.kind;
+    texs[i].noise_type = t.noise_type;
+    texs[i].scale = t.scale;
     for (int b = 0; b < kBins; ++b) {
       texs[i].spec[b] = spectrum_bin(t.rgb, b);
       texs[i].spec_even[b] = t.kind == YART_TEX_CHECKER ? spectrum_bin(t.rgb_even, b) : 0.0;
@@ -234,6 +248,9 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   HIP_TRY(upload(s->owned, objs.data(), objs.size(), &ds.objects, bytes), "upload objects");
   HIP_TRY(upload(s->owned, lights.data(), lights.size(), &ds.lights, bytes), "upload lights");
   HIP_TRY(upload(s->owned, mats.data(), mats.size(), &ds.materials, bytes), "upload materials");
+  for (uint32_t i = 0; i < d->n_textures; ++i)
+    if (d->textures[i].kind == YART_TEX_NOISE)
+      HIP_TRY(upload(s->owned, d->textures[i].perlin, 1, &texs[i].perlin, bytes), "upload Perlin tables");
   HIP_TRY(upload(s->owned, texs.data(), texs.size(), &ds.textures, bytes), "upload textures");
   HIP_TRY(upload(s->owned, bg, kBins, &ds.background, bytes), "upload background");
   std::vector<DevMesh> dm(d->n_meshes);
@@ -256,6 +273,10 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
   ds.has_mesh = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
+  ds.has_ext = 0;
+  for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_ext |= d->objects[i].n_xforms && d->objects[i].xforms[0].kind == YART_XF_MEDIUM;
+  for (uint32_t i = 0; i < d->n_materials; ++i) ds.has_ext |= d->materials[i].kind == YART_MAT_ISOTROPIC;
+  for (uint32_t i = 0; i < d->n_textures; ++i) ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE;
 
   yart_scene_info& in = s->info;
   in.device = device; in.n_objects = d->n_objects; in.n_lights = d->n_lights; in.n_meshes = d->n_meshes;

@@ -16,6 +16,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/yart.h"
+
 namespace yart_dev {
 
 constexpr int kMaxXforms = 4;
@@ -36,9 +38,11 @@ struct DevMaterial {
 };
 
 struct DevTexture {
-  uint32_t kind, reserved;
-  double spec[kBins];       // SOLID / CHECKER odd
+  uint32_t kind, noise_type;
+  double spec[kBins];       // SOLID / CHECKER odd / NOISE: RGB(1,1,1) (texture.rs:272-296)
   double spec_even[kBins];  // CHECKER even
+  double scale;             // NOISE
+  const yart_perlin* perlin;  // NOISE: device copy of the tables
 };
 
 struct alignas(16) DevNode {
@@ -84,6 +88,7 @@ struct DevScene {
   const uint32_t* world_objs;
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
   uint32_t has_mesh;
+  uint32_t has_ext;  // noise textures, isotropic materials or media present (EXT kernels)
   uint32_t n_world_nodes;
 };
 

@@ -96,9 +96,64 @@ __device__ __forceinline__ void sincos_det(double x, double& s, double& c) {
 __device__ __forceinline__ double sin_det(double x) { double s, c; sincos_det(x, s, c); return s; }
 __device__ __forceinline__ double powi5(double x) { double x2 = x * x; return x * (x2 * x2); }  // material.rs:210
 
+// Deterministic natural log, bitwise oracle_log (oracle.c): fdlibm's __ieee754_log.
+__device__ __forceinline__ double log_det(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+               Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+  uint64_t bits = (uint64_t)__double_as_longlong(x);
+  int32_t hx = (int32_t)(bits >> 32);
+  const uint32_t lx = (uint32_t)bits;
+  int k = 0;
+  if (hx < 0x00100000) {
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -INFINITY;
+    if (hx < 0) return NAN;
+    k -= 54; x *= two54;
+    bits = (uint64_t)__double_as_longlong(x); hx = (int32_t)(bits >> 32);
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  int32_t i = (hx + 0x95f64) & 0x100000;
+  bits = (uint64_t)__double_as_longlong(x);
+  bits = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (bits & 0xffffffffull);
+  x = __longlong_as_double((long long)bits);
+  k += (i >> 20);
+  double f = x - 1.0, dk, R;
+  if ((0x000fffff & (2 + hx)) < 3) {
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      dk = (double)k;
+      return dk * ln2_hi + dk * ln2_lo;
+    }
+    R = f * f * (0.5 - 0.33333333333333333 * f);
+    if (k == 0) return f - R;
+    dk = (double)k;
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f);
+  dk = (double)k;
+  const double z = s * s;
+  i = hx - 0x6147a;
+  const double w = z * z;
+  const int32_t j = 0x6b851 - hx;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  i |= j;
+  R = t2 + t1;
+  if (i > 0) {
+    const double hfsq = 0.5 * f * f;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  if (k == 0) return f - s * (f - R);
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
 // ---------------------------------------------------------------- RNG (Philox4x32-10)
-// Counter (block, sample, pixel, phase << 1 | stream), key = seed; oracle.c states the stream
-// layout. A path's draws come in phases — phase 0 the camera ray, phase k the scatter at the k-th
+// Counter (block, sample, pixel, phase << 2 | stream), key = seed; oracle.c states the stream
+// layout (stream 0 path draws, 1 scene construction, 2 ConstantMedium free paths). A path's draws come in phases — phase 0 the camera ray, phase k the scatter at the k-th
 // bounce — each starting at block 0, so k_render computes an iteration's first two blocks at
 // ONE place for the whole wave (rng_phase) instead of at every draw site any lane reaches with
 // an empty buffer. The buffer is consumed by shifting, which in straight-line code is register
@@ -124,7 +179,7 @@ __device__ __forceinline__ void philox(const Rng& r, uint32_t blk, uint32_t& o0,
 }
 // Start `phase` of (pixel, sample) with blocks 0 and 1 in the buffer (4 draws).
 __device__ __forceinline__ void rng_phase(Rng& r, uint32_t pixel, uint32_t sample, uint32_t phase) {
-  r.c1 = sample; r.c2 = pixel; r.c3 = phase << 1;
+  r.c1 = sample; r.c2 = pixel; r.c3 = phase << 2;
   philox(r, 0u, r.b0, r.b1, r.b2, r.b3);
   philox(r, 1u, r.b4, r.b5, r.b6, r.b7);
   r.c0 = 2; r.have = 4;
@@ -148,6 +203,18 @@ __device__ __forceinline__ uint64_t rng_u64(Rng& r) {
   return v;
 }
 __device__ __forceinline__ double gen_f64(Rng& r) { return (double)(rng_u64(r) >> 11) * 0x1.0p-53; }
+
+// Where a world query happens; keys ConstantMedium's draw (stream 2): one gen::<f64>() per medium
+// and query, counter (object index, sample, pixel, segment << 2 | 2), so the draw does not depend
+// on the order objects are tested in.
+struct QueryCtx { uint32_t k0, k1, sample, pixel, seg; };
+__device__ __forceinline__ double medium_draw(const QueryCtx& q, uint32_t obj) {
+  Rng r;
+  r.k0 = q.k0; r.k1 = q.k1; r.c1 = q.sample; r.c2 = q.pixel; r.c3 = (q.seg << 2) | 2u;
+  uint32_t o0, o1, o2, o3;
+  philox(r, obj, o0, o1, o2, o3);
+  return (double)(((((uint64_t)o1) << 32) | o0) >> 11) * 0x1.0p-53;
+}
 __device__ __forceinline__ double gen_range(Rng& r, double low, double high) {  // rand 0.8.5 sample_single
   double scale = high - low;
   for (int guard = 0; guard < 64; ++guard) {
@@ -271,8 +338,8 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
   const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
   const float m = (B + O) * 0x1p-12f;
   float lo = (float)tmin, hi = (float)tmax;
-  lo = lo - fabsf(lo) * 0x1p-10f;
-  hi = hi + fabsf(hi) * 0x1p-10f;
+  if (fabsf(lo) < INFINITY) lo = lo - fabsf(lo) * 0x1p-10f;  // an infinite bound stays as it is
+  if (fabsf(hi) < INFINITY) hi = hi + fabsf(hi) * 0x1p-10f;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     if (!(fabsf(d[j]) >= 1.0e-20f)) continue;  // slab unconstrained
@@ -488,9 +555,35 @@ __device__ __forceinline__ Ray to_local(const DevObject& o, uint32_t nxf, const 
 // id, and hit_record then builds the one record the reference keeps — the winner's, with its
 // wrappers undone innermost first on the way out. Building a record per candidate instead
 // cost every wave the selects and point/normal arithmetic of each primitive some lane hit.
+// ConstantMedium::hit (hittable.rs:277-318): the boundary (the wrapper chain below the medium
+// and the primitive) hit twice, the entry/exit clamped to [t_min, t_max] and 0, and a free path
+// -1/density · ln(ξ) against the distance inside. xf[0][0] holds -1/density.
 template <bool HAS_MESH, bool STATS>
+__device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& lr, const Ray& r,
+                                         double tmin, double tmax, double& t, uint32_t* stk, Stats& st,
+                                         const QueryCtx& q, uint32_t obj) {
+  double t1, t2, u, v;
+  uint32_t sub;
+  if (!prim_t<HAS_MESH, STATS>(S, o, kind, lr, -INFINITY, INFINITY, t1, sub, u, v, stk, st)) return false;
+  if (!prim_t<HAS_MESH, STATS>(S, o, kind, lr, t1 + 0.0001, INFINITY, t2, sub, u, v, stk, st)) return false;
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (!(t1 < t2)) return false;
+  if (t1 < 0.0) t1 = 0.0;
+  const double ray_length = len(r.d);
+  const double distance_inside_boundary = (t2 - t1) * ray_length;
+  const double hit_distance = o.xf[0][0] * log_det(medium_draw(q, obj));
+  if (!(hit_distance < distance_inside_boundary)) return false;
+  t = t1 + hit_distance / ray_length;
+  return true;
+}
+
+// EXT: the scene has media / noise textures / isotropic materials (DevScene::has_ext); kernels
+// for the other scenes are built without those paths (they cost the cornell box 12 % as
+// dead-but-compiled code: registers and spills).
+template <bool HAS_MESH, bool STATS, bool EXT>
 __device__ __forceinline__ bool world_closest(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
-                                              uint32_t* stk, Stats& st) {
+                                              uint32_t* stk, Stats& st, const QueryCtx& q) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -500,7 +593,10 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, const Ray& r, d
     const Ray lr = to_local(o, nxf, r);
     double t, u = 0.0, v = 0.0;
     uint32_t sub = 0;
-    if (prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st)) {
+    const bool hit = (EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM)
+                         ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                         : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+    if (hit) {
       closest = t;
       id.obj = i; id.sub = sub; id.u = u; id.v = v;
       found = true;
@@ -510,10 +606,14 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, const Ray& r, d
   return found;
 }
 
-template <bool HAS_MESH>
+template <bool HAS_MESH, bool EXT>
 __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, const HitId& id, Hit& h) {
   const DevObject& o = S.objects[id.obj];  // per lane
   const uint32_t kind = o.kind, nxf = o.n_xf;
+  if (EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM) {  // hittable.rs:306-315: at t on the outer ray
+    h.t = id.t; h.p = at(r, id.t); h.n = mk(1.0, 0.0, 0.0); h.ff = true; h.mat = o.material;
+    return;
+  }
   const Ray lr = to_local(o, nxf, r);
   if (kind == YART_PRIM_SPHERE) {
     sphere_rec(o.p, lr, id.t, h);
@@ -558,7 +658,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
-  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS>(S, r, tmin, tmax, id, stk, st);
+  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS, false>(S, r, tmin, tmax, id, stk, st, QueryCtx{});
   float inv[3];
   bool use[3];
 #pragma unroll
@@ -635,16 +735,16 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT>
 __device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, Stats& st) {
+                                          int32_t& which, uint32_t* stk, Stats& st, const QueryCtx& q) {
   HitId id;
-  if constexpr (BVH) {
+  if constexpr (BVH) {  // no media in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS>(S, r, tmin, tmax, id, stk, st)) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT>(S, r, tmin, tmax, id, stk, st, q)) return false;
   }
-  hit_record<HAS_MESH>(S, r, id, rec);
+  hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
   return true;
 }
@@ -718,9 +818,68 @@ __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g
 }
 
 // ---------------------------------------------------------------------- materials
+// Rust `f as i32`: saturating, NaN -> 0.
+__device__ __forceinline__ int32_t sat_i32(double f) {
+  if (f != f) return 0;
+  if (f >= 2147483647.0) return INT32_MAX;
+  if (f <= -2147483648.0) return INT32_MIN;
+  return (int32_t)f;
+}
+// Perlin::noise (texture.rs:114-180), as oracle.c's perlin_noise.
+__device__ __noinline__ double perlin_noise(const yart_perlin* P, uint32_t type, V3 p) {
+  if (type == YART_NOISE_SQUARE) {
+    const int32_t i = sat_i32(4.0 * p.x) & 255, j = sat_i32(4.0 * p.y) & 255, k = sat_i32(4.0 * p.z) & 255;
+    return P->ranfloat[P->perm_x[i] ^ P->perm_y[j] ^ P->perm_z[k]];
+  }
+  double u = p.x - floor(p.x), v = p.y - floor(p.y), w = p.z - floor(p.z);
+  const uint32_t i = (uint32_t)sat_i32(floor(p.x)), j = (uint32_t)sat_i32(floor(p.y)), k = (uint32_t)sat_i32(floor(p.z));
+  double accum = 0.0;
+  if (type == YART_NOISE_TRILINEAR) {
+    u = u * u * (3.0 - 2.0 * u);
+    v = v * v * (3.0 - 2.0 * v);
+    w = w * w * (3.0 - 2.0 * w);
+    for (uint32_t di = 0; di < 2; ++di)
+      for (uint32_t dj = 0; dj < 2; ++dj)
+        for (uint32_t dk = 0; dk < 2; ++dk) {  // trilinear_interp texture.rs:192-207
+          const double c = P->ranfloat[P->perm_x[(i + di) & 255u] ^ P->perm_y[(j + dj) & 255u] ^ P->perm_z[(k + dk) & 255u]];
+          accum += ((double)di * u + (double)(1u - di) * (1.0 - u)) * ((double)dj * v + (double)(1u - dj) * (1.0 - v)) *
+                   ((double)dk * w + (double)(1u - dk) * (1.0 - w)) * c;
+        }
+    return accum;
+  }
+  const double uu = u * u * (3.0 - 2.0 * u), vv = v * v * (3.0 - 2.0 * v), ww = w * w * (3.0 - 2.0 * w);
+  for (uint32_t di = 0; di < 2; ++di)
+    for (uint32_t dj = 0; dj < 2; ++dj)
+      for (uint32_t dk = 0; dk < 2; ++dk) {  // perlin_interp texture.rs:209-228
+        const double* c = P->ranvec[P->perm_x[(i + di) & 255u] ^ P->perm_y[(j + dj) & 255u] ^ P->perm_z[(k + dk) & 255u]];
+        const V3 weight_v = mk(u - (double)di, v - (double)dj, w - (double)dk);
+        accum += ((double)di * uu + (1.0 - (double)di) * (1.0 - uu)) * ((double)dj * vv + (1.0 - (double)dj) * (1.0 - vv)) *
+                 ((double)dk * ww + (1.0 - (double)dk) * (1.0 - ww)) * dot(weight_v, ld3(c));
+      }
+  return accum;
+}
+__device__ __forceinline__ double perlin_turb(const yart_perlin* P, uint32_t type, V3 p, int depth) {  // texture.rs:230-242
+  double accum = 0.0, weight = 1.0;
+  V3 temp_p = p;
+  for (int d = 0; d < depth; ++d) {
+    accum += weight * perlin_noise(P, type, temp_p);
+    weight *= 0.5;
+    temp_p = muls(temp_p, 2.0);
+  }
+  return fabs(accum);
+}
+
+template <bool EXT>
 __device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, double wl, V3 p) {
   const DevTexture& t = S.textures[ti];
   const int bin = spectrum_bin(wl);
+  if (EXT && t.kind == YART_TEX_NOISE) {  // NoiseTexture::value texture.rs:265-300 (spec = RGB(1,1,1))
+    const double white = t.spec[bin];
+    if (t.noise_type == YART_NOISE_NET) return white * perlin_turb(t.perlin, t.noise_type, muls(p, t.scale), 7);
+    if (t.noise_type == YART_NOISE_MARBLE)
+      return white * 0.5 * (1.0 + sin_det(t.scale * p.z + 10.0 * perlin_turb(t.perlin, t.noise_type, p, 7)));
+    return white * 0.5 * (1.0 + perlin_noise(t.perlin, t.noise_type, muls(p, t.scale)));
+  }
   if (t.kind == YART_TEX_CHECKER) {  // texture.rs:58-67
     const double sines = sin_det(10.0 * p.x) * sin_det(10.0 * p.y) * sin_det(10.0 * p.z);
     return sines < 0.0 ? t.spec[bin] : t.spec_even[bin];
@@ -774,10 +933,10 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 // wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
 // no lane idles while another still has samples of its own pixel left. Safe because each
 // (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
-template <bool HAS_MESH, bool BVH, bool STATS, bool DYN>
 #ifndef YART_MESH_WAVES_PER_EU
 #define YART_MESH_WAVES_PER_EU 4  // 128 VGPRs; traversal is latency-bound: +36% on david over 2
 #endif
+template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
 __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[(HAS_MESH || BVH) ? 4 * kStackSlots * 64 : 1];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -879,7 +1038,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       const DevMaterial& m = S.materials[hmat];
       const uint32_t kind = m.kind;
       if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-        const double att = texture_value(S, m.texture, ray.wl, hp);
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
         const Onb uvw = onb_from_w(hn);
         V3 dir;
         double pdf_val;
@@ -911,6 +1070,18 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           ray.d = dir;
           depth--;
         }
+      } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
+        V3 p;
+        for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+          const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+          p = mk(px, py, pz);
+          if (!(len2(p) >= 1.0)) break;
+        }
+        T = T * att;
+        ray.o = hp;
+        ray.d = p;
+        depth--;
       } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
         const V3 reflected = reflect(unit(ray.d), hn);
         V3 p;
@@ -919,7 +1090,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           p = mk(px, py, pz);
           if (!(len2(p) >= 1.0)) break;
         }
-        const double att = texture_value(S, m.texture, ray.wl, hp);
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
         T = T * att;
         ray.o = hp;
         ray.d = add(reflected, smul(m.fuzz, p));
@@ -967,21 +1138,23 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           Hit h2; int32_t w2;
           const uint32_t z = opaque_zero();
           Ray r2 = ray; r2.o.x = r2.o.x + (double)z;
-          if (world_hit<HAS_MESH, BVH, STATS>(S, r2, 0.001, INFINITY, h2, w2, stk, st) && z) A.out[w2] = h2.t;
+          if (world_hit<HAS_MESH, BVH, STATS, EXT>(S, r2, 0.001, INFINITY, h2, w2, stk, st, QueryCtx{}) && z) A.out[w2] = h2.t;
         }
 #endif
-        if (!world_hit<HAS_MESH, BVH, STATS>(S, ray, 0.001, INFINITY, h, which, stk, st)) {
+        const QueryCtx q{g.k0, g.k1, smp, pixel, A.max_depth - depth + 1u};
+        if (!world_hit<HAS_MESH, BVH, STATS, EXT>(S, ray, 0.001, INFINITY, h, which, stk, st, q)) {
           const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
           R = T * S.background[bin];
           term = true;
         } else {
           const DevMaterial& m = S.materials[h.mat];
           const uint32_t kind = m.kind;
-          if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC) {
+          if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC ||
+              (EXT && kind == YART_MAT_ISOTROPIC)) {
             hp = h.p; hn = h.n; hmat = h.mat;  // scattered at the top of the next iteration
           } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
             double emitted = 0.0;
-            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value(S, m.texture, ray.wl, h.p);
+            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, ray.wl, h.p);
             R = T * emitted;
             term = true;
           }
@@ -1056,8 +1229,9 @@ __global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevSc
   Stats st;
   double* o = hits + 8 * (size_t)i;
   uint32_t* stk = &s_stack[wave * kStackSlots * 64 + lane];
-  const bool hit = S.world_nodes ? world_hit<false, true, false>(S, r, q[6], q[7], h, which, stk, st)
-                                 : world_hit<true, false, false>(S, r, q[6], q[7], h, which, stk, st);
+  const QueryCtx qc{0u, 0u, 0u, i, 0u};  // a medium's draw for query i: seed 0, sample 0, pixel i
+  const bool hit = S.world_nodes ? world_hit<false, true, false, false>(S, r, q[6], q[7], h, which, stk, st, qc)
+                                 : world_hit<true, false, false, true>(S, r, q[6], q[7], h, which, stk, st, qc);
   if (hit) {
     o[0] = h.t; o[1] = h.p.x; o[2] = h.p.y; o[3] = h.p.z;
     o[4] = h.n.x; o[5] = h.n.y; o[6] = h.n.z; o[7] = h.ff ? 1.0 : 0.0;
@@ -1113,6 +1287,7 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
     case 1: out[i] = a[i] / b[i]; break;
     case 2: sincos_det(a[i], s, c); out[i] = s; break;
     case 3: sincos_det(a[i], s, c); out[i] = c; break;
+    case 5: out[i] = log_det(a[i]); break;
     default: out[i] = pow(a[i], b[i]); break;
   }
 }
@@ -1129,19 +1304,20 @@ hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hip
   const uint32_t units = a.n_blocks * a.n_chunks;
   const uint32_t grid = ((dyn && a.waves < units ? a.waves : units) + 3) / 4;
   if (grid == 0) return hipSuccess;
+#define YART_LAUNCH(MESH, BVH, EXT)                                                                            \
+  do {                                                                                                        \
+    if (stats) hipLaunchKernelGGL((k_render<MESH, BVH, true, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);  \
+    else if (dyn) hipLaunchKernelGGL((k_render<MESH, BVH, false, true, EXT>), dim3(grid), dim3(256), 0, stream, s, a); \
+    else hipLaunchKernelGGL((k_render<MESH, BVH, false, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);        \
+  } while (0)
   if (s.has_mesh) {
-    if (stats) hipLaunchKernelGGL((k_render<true, false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
-    else if (dyn) hipLaunchKernelGGL((k_render<true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<true, false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (s.has_ext) YART_LAUNCH(true, false, true); else YART_LAUNCH(true, false, false);
   } else if (s.world_nodes) {
-    if (stats) hipLaunchKernelGGL((k_render<false, true, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
-    else if (dyn) hipLaunchKernelGGL((k_render<false, true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<false, true, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (s.has_ext) YART_LAUNCH(false, true, true); else YART_LAUNCH(false, true, false);  // noise textures only
   } else {
-    if (stats) hipLaunchKernelGGL((k_render<false, false, true, false>), dim3(grid), dim3(256), 0, stream, s, a);
-    else if (dyn) hipLaunchKernelGGL((k_render<false, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
-    else hipLaunchKernelGGL((k_render<false, false, false, false>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (s.has_ext) YART_LAUNCH(false, false, true); else YART_LAUNCH(false, false, false);
   }
+#undef YART_LAUNCH
   return hipGetLastError();
 }
 hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,

@@ -55,6 +55,46 @@ HittableList two_spheres() {  // scenes.rs:97-118
   return objects;
 }
 
+HittableList two_perlin_spheres(SceneRng& rng) {  // scenes.rs:120-138
+  HittableList objects;
+  objects.add_object(make_shared<StillSphere>(Vec3(0.0, -1000.0, 0.0), 1000.0,
+                                              Lambertian(NoiseTexture(YART_NOISE_MARBLE, 4.0, rng))));
+  objects.add_object(make_shared<StillSphere>(Vec3(0.0, 2.0, 0.0), 2.0, Lambertian(NoiseTexture(YART_NOISE_MARBLE, 4.0, rng))));
+  return objects;
+}
+
+HittableList simple_light(SceneRng& rng) {  // scenes.rs:151-169
+  HittableList objects = two_perlin_spheres(rng);
+  auto difflight = DiffuseLight(SolidColor(RGB(4.0, 4.0, 4.0)));
+  objects.add_object(make_shared<XYRect>(3.0, 5.0, 1.0, 3.0, -2.0, difflight));
+  return objects;
+}
+
+HittableList cornell_box_smoke() {  // scenes.rs:245-318
+  HittableList objects;
+  auto red = Lambertian(SolidColor(RGB(0.65, 0.05, 0.05)));
+  auto white = Lambertian(SolidColor(RGB(0.73, 0.73, 0.73)));
+  auto green = Lambertian(SolidColor(RGB(0.12, 0.45, 0.15)));
+  auto light = DiffuseLight(SolidColor(RGB(7.0, 7.0, 7.0)));
+  objects.add_object(make_shared<YZRect>(0.0, 555.0, 0.0, 555.0, 555.0, green));
+  objects.add_object(make_shared<YZRect>(0.0, 555.0, 0.0, 555.0, 0.0, red));
+  objects.add_object(make_shared<FlipFace>(make_shared<XZRect>(113.0, 443.0, 127.0, 432.0, 554.0, light)));
+  objects.add_object(make_shared<XZRect>(0.0, 555.0, 0.0, 555.0, 0.0, white));
+  objects.add_object(make_shared<XZRect>(0.0, 555.0, 0.0, 555.0, 555.0, white));
+  objects.add_object(make_shared<XYRect>(0.0, 555.0, 0.0, 555.0, 555.0, white));
+  auto box1 = make_shared<ConstantMedium>(
+      make_shared<Translate>(make_shared<RotateY>(make_shared<BoxEntity>(Vec3(0.0, 0.0, 0.0), Vec3(165.0, 330.0, 165.0), white), 15.0),
+                             Vec3(265.0, 0.0, 295.0)),
+      0.01, SolidColor(RGB(0.0, 0.0, 0.0)));
+  auto box2 = make_shared<ConstantMedium>(
+      make_shared<Translate>(make_shared<RotateY>(make_shared<BoxEntity>(Vec3(0.0, 0.0, 0.0), Vec3(165.0, 165.0, 165.0), white), -18.0),
+                             Vec3(130.0, 0.0, 65.0)),
+      0.01, SolidColor(RGB(1.0, 1.0, 1.0)));
+  objects.add_object(box1);
+  objects.add_object(box2);
+  return objects;
+}
+
 HittableList cornell_box() {  // scenes.rs:171-243
   HittableList objects;
   auto red = Lambertian(SolidColor(RGB(0.65, 0.05, 0.05)));
@@ -180,6 +220,25 @@ ScenePreset build_scene_preset(const std::string& name, const std::string& asset
     p.background = RGB(0.7, 0.8, 1.0);
     p.lookfrom = Vec3(13.0, 2.0, 3.0); p.lookat = Vec3(0.0, 0.0, 0.0);
     p.output_filename = "two_spheres.png";
+  } else if (name == "two-perlin-spheres") {
+    SceneRng rng(scene_seed);
+    *world = two_perlin_spheres(rng);
+    p.background = RGB(0.7, 0.8, 1.0);
+    p.lookfrom = Vec3(13.0, 2.0, 30.0); p.lookat = Vec3(0.0, 0.0, 0.0);
+    p.output_filename = "two_perlin_spheres.png";
+  } else if (name == "simple-light") {
+    SceneRng rng(scene_seed);
+    *world = simple_light(rng);
+    p.background = RGB(0.0, 0.0, 0.0);
+    p.lookfrom = Vec3(26.0, 3.0, 6.0); p.lookat = Vec3(0.0, 2.0, 0.0);
+    d.samples_per_pixel = 400;
+    p.output_filename = "simple_light.png";
+  } else if (name == "cornell-box-smoke") {
+    *world = cornell_box_smoke();
+    p.background = RGB(0.0, 0.0, 0.0);
+    p.lookfrom = Vec3(278.0, 278.0, -800.0); p.lookat = Vec3(278.0, 278.0, 0.0);
+    d.width = 600; d.height = 600; d.samples_per_pixel = 200; d.vfov = 40.0;
+    p.output_filename = "cornell_box_smoke.png";
   } else if (name == "cornell-box") {
     *world = cornell_box();
     p.lights.add_object(make_shared<XZRect>(213.0, 343.0, 227.0, 332.0, 554.0, NoMaterial()));
@@ -228,11 +287,10 @@ ScenePreset build_scene_preset(const std::string& name, const std::string& asset
     p.lookfrom = Vec3(50.0, 120.0, 300.0); p.lookat = Vec3(0.0, 120.0, 0.0);
     d.width = 600; d.height = 600; d.samples_per_pixel = 10000; d.vfov = 20.0; d.aperture = 0.001;
     p.output_filename = "david.png";
-  } else if (name == "two-perlin-spheres" || name == "earth" || name == "simple-light" || name == "cornell-box-smoke" ||
-             name == "next-week-final") {
-    // Perlin/image textures, ConstantMedium, MovingSphere and BVHNode are outside this build's
-    // hot-path scope.
-    throw std::invalid_argument("scene `" + name + "` needs features outside this build's scope (SURVEY.md §8f)");
+  } else if (name == "earth" || name == "next-week-final") {
+    // ImageTexture (a JPEG decoded by the `image` crate), MovingSphere and BVHNode are not built
+    // yet.
+    throw std::invalid_argument("scene `" + name + "` needs ImageTexture / MovingSphere / BVHNode, outside this build");
   } else {
     throw std::invalid_argument("invalid value '" + name + "' for '--scene <SCENE>'");
   }

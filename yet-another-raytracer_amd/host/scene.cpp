@@ -32,7 +32,8 @@ const Material SF66 = Dielectric(2.0245976, 0.470187196, 2.59970433, 0.014705322
 
 // ------------------------------------------------------------------------ flattening
 static bool same_texture(const yart_texture& a, const Texture& t) {
-  return a.kind == t.kind && !std::memcmp(a.rgb, t.a.e, sizeof a.rgb) && !std::memcmp(a.rgb_even, t.b.e, sizeof a.rgb_even);
+  return a.kind == t.kind && !std::memcmp(a.rgb, t.a.e, sizeof a.rgb) && !std::memcmp(a.rgb_even, t.b.e, sizeof a.rgb_even) &&
+         a.noise_type == t.noise_type && a.scale == t.scale && a.perlin == t.perlin.get();
 }
 uint32_t Flattener::texture(const Texture& t) {
   for (size_t i = 0; i < out_.textures.size(); ++i)
@@ -41,13 +42,20 @@ uint32_t Flattener::texture(const Texture& t) {
   y.kind = t.kind;
   std::memcpy(y.rgb, t.a.e, sizeof y.rgb);
   std::memcpy(y.rgb_even, t.b.e, sizeof y.rgb_even);
+  y.noise_type = t.noise_type;
+  y.scale = t.scale;
+  if (t.perlin) {
+    out_.perlins.push_back(t.perlin);
+    y.perlin = t.perlin.get();
+  }
   out_.textures.push_back(y);
   return (uint32_t)(out_.textures.size() - 1);
 }
 uint32_t Flattener::material(const Material& m) {
   yart_material y{};
   y.kind = m.kind;
-  y.texture = (m.kind == YART_MAT_LAMBERTIAN || m.kind == YART_MAT_METAL || m.kind == YART_MAT_DIFFUSE_LIGHT) ? texture(m.texture) : 0;
+  y.texture = (m.kind == YART_MAT_LAMBERTIAN || m.kind == YART_MAT_METAL || m.kind == YART_MAT_DIFFUSE_LIGHT ||
+               m.kind == YART_MAT_ISOTROPIC) ? texture(m.texture) : 0;
   y.fuzz = m.fuzz;
   for (int i = 0; i < 3; ++i) { y.b[i] = m.b[i]; y.c[i] = m.c[i]; }
   for (size_t i = 0; i < out_.materials.size(); ++i)
@@ -72,7 +80,8 @@ void Flattener::emit(uint32_t kind, uint32_t material, const std::vector<yart_xf
   if (chain.size() > YART_MAX_XFORMS) throw std::runtime_error("more than YART_MAX_XFORMS nested wrappers");
   yart_object o{};
   o.kind = kind;
-  o.material = material;
+  o.material = override_ ? this->material(*override_) : material;
+  if (override_) override_count_++;
   o.mesh = mesh;
   o.n_xforms = (uint32_t)chain.size();
   for (size_t i = 0; i < chain.size(); ++i) o.xforms[i] = chain[i];
@@ -128,6 +137,42 @@ void FlipFace::flatten(Flattener& f, std::vector<yart_xform>& chain) const {
   chain.push_back(x);
   inner->flatten(f, chain);
   chain.pop_back();
+}
+
+void ConstantMedium::flatten(Flattener& f, std::vector<yart_xform>& chain) const {
+  if (!chain.empty()) throw std::runtime_error("ConstantMedium under another wrapper is not supported");
+  yart_xform x{};
+  x.kind = YART_XF_MEDIUM;
+  x.v[0] = density;
+  chain.push_back(x);
+  f.override_material(&phase_function);
+  boundary->flatten(f, chain);
+  const uint32_t n = f.override_count();
+  f.override_material(nullptr);
+  chain.pop_back();
+  if (n != 1) throw std::runtime_error("a ConstantMedium boundary must be one primitive");
+}
+
+Texture NoiseTexture(uint32_t noise_type, double scale, SceneRng& rng) {
+  auto P = std::make_shared<yart_perlin>();
+  for (int i = 0; i < 256; ++i) P->ranfloat[i] = rng.gen_range(0.0, 1.0);  // texture.rs:99-101
+  for (int i = 0; i < 256; ++i)                                             // Vec3::random(-1, 1)
+    for (int k = 0; k < 3; ++k) P->ranvec[i][k] = rng.gen_range(-1.0, 1.0);
+  int32_t* perms[3] = {P->perm_x, P->perm_y, P->perm_z};
+  for (int32_t* p : perms) {  // perlin_generate_perm + permute (texture.rs:182-190)
+    for (int i = 0; i < 256; ++i) p[i] = i;
+    for (int i = 255; i >= 1; --i) {
+      const uint64_t target = rng.gen_index((uint64_t)i);
+      std::swap(p[i], p[target]);
+    }
+  }
+  Texture t;
+  t.kind = YART_TEX_NOISE;
+  t.a = RGB(1.0, 1.0, 1.0);  // the RGB::new(1, 1, 1) it reflects (texture.rs:272-296)
+  t.noise_type = noise_type;
+  t.scale = scale;
+  t.perlin = P;
+  return t;
 }
 
 yart_scene_desc SceneDesc::desc() const {
@@ -295,6 +340,14 @@ uint64_t SceneRng::next_u64() {
   return ((uint64_t)buf_[2 * i + 1] << 32) | buf_[2 * i];
 }
 double SceneRng::gen_f64() { return (double)(next_u64() >> 11) * 0x1.0p-53; }
+uint64_t SceneRng::gen_index(uint64_t n) {  // UniformInt<usize>::sample_single(0..n): zone rejection
+  const uint64_t zone = (n << __builtin_clzll(n)) - 1;
+  for (;;) {
+    const uint64_t v = next_u64();
+    const unsigned __int128 m = (unsigned __int128)v * n;
+    if ((uint64_t)m <= zone) return (uint64_t)(m >> 64);
+  }
+}
 double SceneRng::gen_range(double low, double high) {
   double scale = high - low;
   for (;;) {

@@ -32,12 +32,19 @@ struct Vec3 {  // vec3.rs:13-247 (host-side values only)
 using RGB = Vec3;  // color.rs:25-28 (same layout, RGB channels)
 
 // ------------------------------------------------------------------ textures (texture.rs)
+class SceneRng;
 struct Texture {
   uint32_t kind = YART_TEX_SOLID;
   RGB a, b;
+  uint32_t noise_type = 0;
+  double scale = 0.0;
+  std::shared_ptr<const yart_perlin> perlin;  // NOISE: its own tables (Perlin::new per texture)
 };
-inline Texture SolidColor(RGB c) { return Texture{YART_TEX_SOLID, c, RGB()}; }                 // texture.rs:18-40
-inline Texture CheckerTexture(RGB odd, RGB even) { return Texture{YART_TEX_CHECKER, odd, even}; }  // texture.rs:42-68
+inline Texture SolidColor(RGB c) { Texture t; t.kind = YART_TEX_SOLID; t.a = c; return t; }       // texture.rs:18-40
+inline Texture CheckerTexture(RGB odd, RGB even) { Texture t; t.kind = YART_TEX_CHECKER; t.a = odd; t.b = even; return t; }  // texture.rs:42-68
+// NoiseTexture::new (texture.rs:251-260): Perlin::new draws its tables from thread_rng in the
+// reference; here from the scene's seeded stream, in the same order (ranfloat, ranvec, perm_x/y/z).
+Texture NoiseTexture(uint32_t noise_type, double scale, SceneRng& rng);
 
 // ----------------------------------------------------------------- materials (material.rs)
 struct Material {
@@ -50,6 +57,7 @@ inline Material Lambertian(Texture t) { Material m; m.kind = YART_MAT_LAMBERTIAN
 inline Material Metal(Texture t, double fuzz) { Material m; m.kind = YART_MAT_METAL; m.texture = t; m.fuzz = fuzz; return m; }
 inline Material DiffuseLight(Texture t) { Material m; m.kind = YART_MAT_DIFFUSE_LIGHT; m.texture = t; return m; }
 inline Material NoMaterial() { return Material{}; }
+inline Material Isotropic(Texture t) { Material m; m.kind = YART_MAT_ISOTROPIC; m.texture = t; return m; }  // material.rs:357-381
 Material Dielectric(double b1, double b2, double b3, double c1, double c2, double c3);
 // Glass presets, material.rs:121-185 (C in nm^2).
 extern const Material BAF10, BK7, SF11, FK51A, LASF9, SF66;
@@ -153,6 +161,15 @@ class FlipFace : public Hittable {  // hittable.rs:328-354
   HittablePtr inner;
   void flatten(Flattener& f, std::vector<yart_xform>& chain) const override;
 };
+// ConstantMedium (hittable.rs:258-326): a boundary of ONE primitive (under its own wrappers) and
+// an Isotropic phase function; flattened as that primitive with an outermost MEDIUM wrapper.
+class ConstantMedium : public Hittable {
+ public:
+  ConstantMedium(HittablePtr boundary, double density, Texture t)
+      : boundary(std::move(boundary)), density(density), phase_function(Isotropic(t)) {}
+  HittablePtr boundary; double density; Material phase_function;
+  void flatten(Flattener& f, std::vector<yart_xform>& chain) const override;
+};
 
 // Owns every array a yart_scene_desc points into.
 class SceneDesc {
@@ -161,6 +178,7 @@ class SceneDesc {
   std::vector<yart_material> materials;
   std::vector<yart_texture> textures;
   std::vector<std::shared_ptr<const MeshData>> mesh_data;
+  std::vector<std::shared_ptr<const yart_perlin>> perlins;  // tables the noise textures point at
   std::vector<yart_mesh> meshes;
   double background[3] = {0, 0, 0};
   yart_scene_desc desc() const;
@@ -174,8 +192,13 @@ class Flattener {
   uint32_t mesh(const std::shared_ptr<const MeshData>& m);
   void emit(uint32_t kind, uint32_t material, const std::vector<yart_xform>& chain, const double* p, int np,
             uint32_t mesh = 0);
+  // While set, emitted primitives take this material (a medium's phase function) and are counted.
+  void override_material(const Material* m) { override_ = m; override_count_ = 0; }
+  uint32_t override_count() const { return override_count_; }
 
  private:
+  const Material* override_ = nullptr;
+  uint32_t override_count_ = 0;
   uint32_t texture(const Texture& t);
   SceneDesc& out_;
   std::vector<yart_object>* target_ = nullptr;
@@ -212,6 +235,7 @@ class SceneRng {
   explicit SceneRng(uint64_t seed);
   double gen_f64();                       // rng.gen::<f64>()
   double gen_range(double low, double high);  // rng.gen_range(low..high)
+  uint64_t gen_index(uint64_t n);         // rng.gen_range(0..n) for usize (rand 0.8.5 UniformInt)
  private:
   uint64_t next_u64();
   uint32_t key_[2], ctr_[4], buf_[4];

@@ -5,17 +5,24 @@ ABI_VERSION = 1
 
 OK, ERR_INVALID, ERR_DEVICE, ERR_NO_MEMORY, ERR_UNSUPPORTED, ERR_IO = 0, -1, -2, -3, -4, -5
 
-TEX_SOLID, TEX_CHECKER = 0, 1
-MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT = 0, 1, 2, 3, 4
+TEX_SOLID, TEX_CHECKER, TEX_NOISE = 0, 1, 2
+NOISE_SQUARE, NOISE_TRILINEAR, NOISE_SMOOTH, NOISE_MARBLE, NOISE_NET = range(5)
+MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC = 0, 1, 2, 3, 4, 5
 PRIM_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT, PRIM_BOX, PRIM_TRIANGLE, PRIM_MESH = range(7)
-XF_TRANSLATE, XF_ROTATE_Y, XF_FLIP_FACE = 1, 2, 3
+XF_TRANSLATE, XF_ROTATE_Y, XF_FLIP_FACE, XF_MEDIUM = 1, 2, 3, 4
 MAX_XFORMS = 4
 
 D3 = C.c_double * 3
 
 
+class Perlin(C.Structure):
+    _fields_ = [("ranfloat", C.c_double * 256), ("ranvec", (C.c_double * 3) * 256), ("perm_x", C.c_int32 * 256),
+                ("perm_y", C.c_int32 * 256), ("perm_z", C.c_int32 * 256)]
+
+
 class Texture(C.Structure):
-    _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("rgb", D3), ("rgb_even", D3)]
+    _fields_ = [("kind", C.c_uint32), ("noise_type", C.c_uint32), ("rgb", D3), ("rgb_even", D3), ("scale", C.c_double),
+                ("perlin", C.POINTER(Perlin))]
 
 
 class Material(C.Structure):
