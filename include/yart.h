@@ -45,7 +45,8 @@ typedef enum yart_status {
 enum {
   YART_TEX_SOLID = 0,   /* SolidColor<RGB>            texture.rs:18-40   */
   YART_TEX_CHECKER = 1, /* CheckerTexture<RGB>        texture.rs:42-68   */
-  YART_TEX_NOISE = 2    /* NoiseTexture (Perlin)      texture.rs:262-300 */
+  YART_TEX_NOISE = 2,   /* NoiseTexture (Perlin)      texture.rs:262-300 */
+  YART_TEX_IMAGE = 3    /* ImageTexture               texture.rs:302-345 */
 };
 enum { /* NoiseType, texture.rs:70-82 */
   YART_NOISE_SQUARE = 0,
@@ -69,6 +70,9 @@ typedef struct yart_texture {
   double rgb_even[3];        /* CHECKER: the `even` colour.                                */
   double scale;              /* NOISE: NoiseTexture::scale                                 */
   const yart_perlin* perlin; /* NOISE: its tables (copied by yart_scene_create)            */
+  uint32_t width, height;    /* IMAGE: texel grid                                          */
+  const uint8_t* pixels;     /* IMAGE: width*height RGB8 texels, rows top first (to_rgb8);
+                                NULL / empty = the reference's no-data texture (value 1.0) */
 } yart_texture;
 
 /* --------------------------------------------------------------- materials (material.rs) */
@@ -276,7 +280,8 @@ int yart_intersect(yart_scene* scene, const double* rays, uint32_t n, double* hi
 /* The per-sample random stream: n draws of gen::<f64>() for (pixel, sample). */
 int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n,
                    double* out);
-/* Elementwise device math on n inputs: op 0 sqrt(a), 1 a/b, 2 sin(a), 3 cos(a), 4 pow(a,b). */
+/* Elementwise device math on n inputs: op 0 sqrt(a), 1 a/b, 2 sin(a), 3 cos(a), 4 pow(a,b),
+ * 5 ln(a), 6 acos(a), 7 atan2(a,b) (3, 5-7: the deterministic fdlibm forms the kernels use). */
 int yart_probe_math(int device, int op, const double* a, const double* b, uint32_t n,
                     double* out);
 

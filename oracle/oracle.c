@@ -121,6 +121,133 @@ double oracle_cos(double x) {
   }
 }
 
+/* Deterministic acos / atan / atan2 for get_sphere_uv (sphere.rs:213-220), bitwise the device's:
+ * fdlibm's __ieee754_acos, atan and __ieee754_atan2 (Sun, 1993); + - * / and sqrt only. */
+static inline int32_t hi_word(double x) { uint64_t b; memcpy(&b, &x, 8); return (int32_t)(b >> 32); }
+static inline uint32_t lo_word(double x) { uint64_t b; memcpy(&b, &x, 8); return (uint32_t)b; }
+static inline double with_lo_zero(double x) { uint64_t b; memcpy(&b, &x, 8); b &= 0xffffffff00000000ull; memcpy(&x, &b, 8); return x; }
+double oracle_acos(double x) {
+  const double pi = 3.14159265358979311600e+00, pio2_hi = 1.57079632679489655800e+00,
+               pio2_lo = 6.12323399573676603587e-17, pS0 = 1.66666666666666657415e-01,
+               pS1 = -3.25565818622400915405e-01, pS2 = 2.01212532134862925881e-01,
+               pS3 = -4.00555345006794114027e-02, pS4 = 7.91534994289814532176e-04,
+               pS5 = 3.47933107596021167570e-05, qS1 = -2.40339491173441421878e+00,
+               qS2 = 2.02094576023350569471e+00, qS3 = -6.88283971605453293030e-01,
+               qS4 = 7.70381505559019352791e-02;
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff;
+  double z, p, q, r, w, s, c, df;
+  if (ix >= 0x3ff00000) {
+    if (((ix - 0x3ff00000) | (int32_t)lo_word(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3fe00000) {
+    if (ix <= 0x3c600000) return pio2_hi + pio2_lo;
+    z = x * x;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  } else if (hx < 0) {
+    z = (1.0 + x) * 0.5;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    s = sqrt(z);
+    r = p / q;
+    w = r * s - pio2_lo;
+    return pi - 2.0 * (s + w);
+  }
+  z = (1.0 - x) * 0.5;
+  s = sqrt(z);
+  df = with_lo_zero(s);
+  c = (z - df * df) / (s + df);
+  p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  r = p / q;
+  w = r * s + c;
+  return 2.0 * (df + w);
+}
+static double det_atan(double x) {
+  static const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                                   1.57079632679489655800e+00};
+  static const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                                   6.12323399573676603587e-17};
+  static const double aT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                                -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                                -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x44100000) {
+    if (ix > 0x7ff00000 || (ix == 0x7ff00000 && lo_word(x) != 0)) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3fdc0000) {
+    if (ix < 0x3e200000) return x;
+    id = -1;
+  } else {
+    x = fabs(x);
+    if (ix < 0x3ff30000) {
+      if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+      else { id = 1; x = (x - 1.0) / (x + 1.0); }
+    } else {
+      if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+      else { id = 3; x = -1.0 / x; }
+    }
+  }
+  const double z = x * x, w = z * z;
+  const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+  const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+  if (id < 0) return x - x * (s1 + s2);
+  const double zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -zz : zz;
+}
+double oracle_atan2(double y, double x) {
+  const double tiny = 1.0e-300, pi_o_4 = 7.8539816339744827900e-01, pi_o_2 = 1.5707963267948965580e+00,
+               pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff, hy = hi_word(y), iy = hy & 0x7fffffff;
+  const uint32_t lx = lo_word(x), ly = lo_word(y);
+  if ((ix | (int32_t)((lx | (0u - lx)) >> 31)) > 0x7ff00000 || (iy | (int32_t)((ly | (0u - ly)) >> 31)) > 0x7ff00000)
+    return x + y;
+  if (((hx - 0x3ff00000) | (int32_t)lx) == 0) return det_atan(y);
+  const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if ((iy | (int32_t)ly) == 0) {
+    switch (m) {
+      case 0: case 1: return y;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if ((ix | (int32_t)lx) == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7ff00000) {
+    if (iy == 0x7ff00000) {
+      switch (m) {
+        case 0: return pi_o_4 + tiny;
+        case 1: return -pi_o_4 - tiny;
+        case 2: return 3.0 * pi_o_4 + tiny;
+        default: return -3.0 * pi_o_4 - tiny;
+      }
+    }
+    switch (m) {
+      case 0: return 0.0;
+      case 1: return -0.0;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if (iy == 0x7ff00000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int k = (iy - ix) >> 20;
+  double z;
+  if (k > 60) z = pi_o_2 + 0.5 * pi_lo;
+  else if (hx < 0 && k < -60) z = 0.0;
+  else z = det_atan(fabs(y / x));
+  switch (m) {
+    case 0: return z;
+    case 1: return -z;  /* the high-word sign flip of fdlibm */
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+  }
+}
+
 /* Deterministic natural log shared bit for bit with the device (libm's log differs between glibc
  * and ROCm's ocml in the last ulp): fdlibm's __ieee754_log (Sun, 1993) — reduction to
  * f in [sqrt(2)/2 - 1, sqrt(2) - 1), s = f / (2 + f), and the Lg1..Lg7 minimax polynomial in s^2.
@@ -374,6 +501,7 @@ struct oracle_scene {
   yart_material* mats; uint32_t nmats;
   yart_texture* texs; uint32_t ntexs;
   yart_perlin* perlins; /* per texture (NOISE) */
+  uint8_t** images;     /* per texture (IMAGE) */
   qbvh_t* meshes; uint32_t nmeshes;
   double background[3];
   /* per object, per wrapper: RotateY sin/cos (hittable.rs:173-176) */
@@ -381,7 +509,7 @@ struct oracle_scene {
   double (*light_sc)[YART_MAX_XFORMS][2];
 };
 
-typedef struct { double t; v3 p, normal; int front_face; uint32_t mat; } hit_rec; /* hittable.rs:37-45 (u, v not read in scope) */
+typedef struct { double u, v, t; v3 p, normal; int front_face; uint32_t mat; } hit_rec; /* hittable.rs:37-45 */
 
 /* ---------------------------------------------------------- L4QBVH build (qbvh.rs:252-361) */
 typedef struct { double min[3], max[3]; } aabb_t; /* aabb.rs:8-12 */
@@ -574,6 +702,7 @@ static int qbvh_hit(const qbvh_t* q, const ray_t* r, double t_min, double t_max,
           t_max = tl[i];
           rec->t = tl[i]; rec->p = V(px[i], py[i], pz[i]); rec->normal = V(nx[i], ny[i], nz[i]);
           rec->front_face = ffl[i];
+          rec->u = 0.0; rec->v = 0.0; /* mesh texcoords: no in-scope texture reads them on a mesh */
           found = 1;
         }
       }
@@ -626,6 +755,10 @@ static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_ma
   if (radius < 0.0) { rec->normal = vneg(outward); rec->front_face = dot(r->d, outward) > 0.0; }
   else { rec->normal = outward; rec->front_face = dot(r->d, outward) < 0.0; }
   rec->t = t; rec->p = pt;
+  /* get_sphere_uv (sphere.rs:213-220) of the outward normal */
+  const double theta = oracle_acos(-outward.y), phi = oracle_atan2(-outward.z, outward.x) + PI;
+  rec->u = phi / (2.0 * PI);
+  rec->v = theta / PI;
   return 1;
 }
 /* aarect.rs: axis a (plane normal), in-plane axes b, c: XY a=z (b=x, c=y) :41-76;
@@ -641,6 +774,8 @@ static int rect_hit(int kind, const double* p, const ray_t* r, double t_min, dou
   double x = comp(r->o, b) + t * comp(r->d, b);
   double y = comp(r->o, c) + t * comp(r->d, c);
   if (x < p[0] || x > p[1] || y < p[2] || y > p[3]) return 0;
+  rec->u = (x - p[0]) / (p[1] - p[0]);
+  rec->v = (y - p[2]) / (p[3] - p[2]);
   rec->t = t; rec->p = ray_at(r, t);
   if (dot(r->d, outward) < 0.0) { rec->normal = outward; rec->front_face = 1; }
   else { rec->normal = vneg(outward); rec->front_face = 0; }
@@ -675,6 +810,8 @@ static int triangle_hit(const double* p, const ray_t* r, double t_min, double t_
   if (t < t_min || t > t_max) return 0;
   double w = 1.0 - u - v;
   v3 outward = vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v));
+  rec->u = p[18] * w + p[20] * u + p[22] * v; /* triangle.rs:93-94 */
+  rec->v = p[19] * w + p[21] * u + p[23] * v;
   rec->t = t; rec->p = ray_at(r, t);
   if (dot(r->d, outward) < 0.0) { rec->normal = outward; rec->front_face = 1; }
   else { rec->normal = vneg(outward); rec->front_face = 0; }
@@ -714,6 +851,7 @@ static int object_hit(const oracle_scene* s, const yart_object* o, const double 
     const double hit_distance = neg_inv_density * oracle_log(medium_draw(cx->seed, obj, cx->sample, cx->pixel, cx->seg));
     if (!(hit_distance < distance_inside_boundary)) return 0;
     rec->t = rec1.t + hit_distance / ray_length;
+    rec->u = 0.0; rec->v = 0.0;
     rec->p = ray_at(r, rec->t);
     rec->normal = V(1.0, 0.0, 0.0);
     rec->front_face = 1;
@@ -847,6 +985,13 @@ static v3 lights_random(const oracle_scene* s, v3 origin, rng_t* g) { /* hittabl
 }
 
 /* ------------------------------------------------------------------ textures / materials */
+/* f64::clamp (propagates NaN) and Rust `f as u32` (saturating, NaN -> 0). */
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static uint32_t sat_u32(double f) {
+  if (!(f > 0.0)) return 0;
+  if (f >= 4294967295.0) return UINT32_MAX;
+  return (uint32_t)f;
+}
 /* Rust `f as i32`: saturating, NaN -> 0. */
 static int32_t sat_i32(double f) {
   if (f != f) return 0;
@@ -902,6 +1047,17 @@ static double perlin_turb(const yart_perlin* P, uint32_t type, v3 p, int depth) 
 
 static double texture_value(const oracle_scene* s, uint32_t ti, const ray_t* r, const hit_rec* rec) {
   const yart_texture* t = &s->texs[ti];
+  if (t->kind == YART_TEX_IMAGE) { /* ImageTexture::value texture.rs:320-344 */
+    if (!t->pixels || t->width == 0 || t->height == 0) return 1.0;
+    const double uu = clampd(rec->u, 0.0, 1.0), vv = 1.0 - clampd(rec->v, 0.0, 1.0);
+    uint32_t i = sat_u32(uu * (double)t->width), j = sat_u32(vv * (double)t->height);
+    if (i >= t->width) i = t->width - 1;
+    if (j >= t->height) j = t->height - 1;
+    const double color_scale = 1.0 / 255.0;
+    const uint8_t* px = &t->pixels[(size_t)j * t->width * 3 + (size_t)i * 3];
+    const double rgb[3] = {color_scale * (double)px[0], color_scale * (double)px[1], color_scale * (double)px[2]};
+    return oracle_rgb_reflect(rgb, r->wl);
+  }
   if (t->kind == YART_TEX_NOISE) { /* NoiseTexture::value texture.rs:265-300 (rgb = white) */
     const double white = oracle_rgb_reflect(t->rgb, r->wl);
     if (t->noise_type == YART_NOISE_NET) return white * perlin_turb(t->perlin, t->noise_type, vmuls(rec->p, t->scale), 7);
@@ -1182,11 +1338,12 @@ int oracle_finalize_rgba8(const double* xyz_sum, uint32_t w, uint32_t h, uint32_
   return YART_OK;
 }
 
-double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3]) {
+double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3], double u, double v) {
   ray_t r = {V(0.0, 0.0, 0.0), V(1.0, 0.0, 0.0), 0.0, wl};
   hit_rec rec;
   memset(&rec, 0, sizeof rec);
   rec.p = V(p[0], p[1], p[2]);
+  rec.u = u; rec.v = v;
   return texture_value(s, tex, &r, &rec);
 }
 
@@ -1244,7 +1401,7 @@ int oracle_scene_create(const yart_scene_desc* d, oracle_scene** out) {
          d->materials[i].texture >= d->n_textures))
       return YART_ERR_INVALID;
   for (uint32_t i = 0; i < d->n_textures; ++i)
-    if (d->textures[i].kind > YART_TEX_NOISE ||
+    if (d->textures[i].kind > YART_TEX_IMAGE ||
         (d->textures[i].kind == YART_TEX_NOISE && (!d->textures[i].perlin || d->textures[i].noise_type > YART_NOISE_NET)))
       return YART_ERR_INVALID;
   for (uint32_t i = 0; i < d->n_objects; ++i)
@@ -1260,8 +1417,16 @@ int oracle_scene_create(const yart_scene_desc* d, oracle_scene** out) {
   if (s->nmats) memcpy(s->mats, d->materials, sizeof(yart_material) * s->nmats);
   if (s->ntexs) memcpy(s->texs, d->textures, sizeof(yart_texture) * s->ntexs);
   s->perlins = (yart_perlin*)calloc(s->ntexs + 1, sizeof(yart_perlin)); /* own copies of the tables */
-  for (uint32_t i = 0; i < s->ntexs; ++i)
+  s->images = (uint8_t**)calloc(s->ntexs + 1, sizeof(uint8_t*));        /* and of the texels */
+  for (uint32_t i = 0; i < s->ntexs; ++i) {
     if (s->texs[i].kind == YART_TEX_NOISE) { s->perlins[i] = *d->textures[i].perlin; s->texs[i].perlin = &s->perlins[i]; }
+    if (s->texs[i].kind == YART_TEX_IMAGE && s->texs[i].pixels && s->texs[i].width && s->texs[i].height) {
+      const size_t n = (size_t)s->texs[i].width * s->texs[i].height * 3;
+      s->images[i] = (uint8_t*)malloc(n);
+      memcpy(s->images[i], d->textures[i].pixels, n);
+      s->texs[i].pixels = s->images[i];
+    }
+  }
   memcpy(s->background, d->background, sizeof(s->background));
   s->obj_sc = calloc(s->nobj + 1, sizeof(*s->obj_sc));
   s->light_sc = calloc(s->nlights + 1, sizeof(*s->light_sc));
@@ -1282,7 +1447,8 @@ void oracle_scene_destroy(oracle_scene* s) {
     qbvh_t* q = &s->meshes[m];
     free(q->vert); free(q->norm); free(q->nodes); free(q->leaves); free(q->leaf_of_first);
   }
-  free(s->meshes); free(s->objects); free(s->lights); free(s->mats); free(s->texs); free(s->perlins);
+  for (uint32_t i = 0; s->images && i < s->ntexs; ++i) free(s->images[i]);
+  free(s->meshes); free(s->objects); free(s->lights); free(s->mats); free(s->texs); free(s->perlins); free(s->images);
   free(s->obj_sc); free(s->light_sc);
   free(s);
 }

@@ -67,8 +67,11 @@ double oracle_gen_range_f64(uint64_t seed, uint32_t pixel, uint32_t sample, doub
 double oracle_sin(double x); /* deterministic sin/cos shared bit-for-bit with the device */
 double oracle_cos(double x);
 double oracle_log(double x); /* deterministic natural log (fdlibm), shared bit-for-bit with the device */
-/* Texture::value of texture `tex` at point p and wavelength wl (known-answer tests). */
-double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3]);
+double oracle_acos(double x); /* deterministic acos / atan2 (fdlibm), likewise */
+double oracle_atan2(double y, double x);
+/* Texture::value of texture `tex` at point p, texture coordinates (u, v) and wavelength wl
+ * (known-answer tests). */
+double oracle_texture_probe(const oracle_scene* s, uint32_t tex, double wl, const double p[3], double u, double v);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,9 @@ def lib():
         "oracle_sin": (D, [D]),
         "oracle_cos": (D, [D]),
         "oracle_log": (D, [D]),
-        "oracle_texture_probe": (D, [P, U32, D, P]),
+        "oracle_texture_probe": (D, [P, U32, D, P, D, D]),
+        "oracle_acos": (D, [D]),
+        "oracle_atan2": (D, [D, D]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -81,9 +83,9 @@ class OracleScene:
         assert rc == 0
         return out
 
-    def texture(self, tex, wl, p):
+    def texture(self, tex, wl, p, u=0.0, v=0.0):
         pt = np.ascontiguousarray(p, dtype=np.float64)
-        return lib().oracle_texture_probe(self._s, tex, wl, _p(pt))
+        return lib().oracle_texture_probe(self._s, tex, wl, _p(pt), u, v)
 
     def intersect(self, rays):
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
@@ -149,6 +151,16 @@ class DescBuilder:
         t.kind, t.noise_type, t.scale = abi.TEX_NOISE, noise_type, scale
         t.rgb = (C.c_double * 3)(1.0, 1.0, 1.0)
         t.perlin = C.pointer(P)
+        self.textures.append(t)
+        return len(self.textures) - 1
+
+    def image_texture(self, rgb8):
+        """An ImageTexture over an (h, w, 3) uint8 array (rows top first)."""
+        px = np.ascontiguousarray(rgb8, dtype=np.uint8)
+        self._keep.append(px)
+        t = abi.Texture()
+        t.kind, t.height, t.width = abi.TEX_IMAGE, px.shape[0], px.shape[1]
+        t.pixels = px.ctypes.data_as(C.POINTER(C.c_uint8))
         self.textures.append(t)
         return len(self.textures) - 1
 

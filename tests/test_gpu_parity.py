@@ -66,6 +66,17 @@ def test_device_log_matches_oracle(dev):
     np.testing.assert_array_equal(_probe(dev, 5, a), np.array([L.oracle_log(x) for x in a]))
 
 
+def test_device_acos_atan2_match_oracle(dev):
+    rng = np.random.default_rng(7)
+    a = np.concatenate([rng.uniform(-1, 1, 50000), [1.0, -1.0, 0.0, -0.0, 0.5, -0.5]])
+    L = O.lib()
+    np.testing.assert_array_equal(_probe(dev, 6, a), np.array([L.oracle_acos(x) for x in a]))
+    y, x = rng.normal(size=(2, 50000)) * 10.0 ** rng.uniform(-5, 5, (2, 50000))
+    y = np.concatenate([y, [0.0, -0.0, 1.0, -1.0]])
+    x = np.concatenate([x, [-1.0, -1.0, 0.0, 0.0]])
+    np.testing.assert_array_equal(_probe(dev, 7, y, x), np.array([L.oracle_atan2(p, q) for p, q in zip(y, x)]))
+
+
 def _hits_equal(h1, o1, h2, o2):
     np.testing.assert_array_equal(o1, o2)
     m = o1 >= 0
@@ -214,6 +225,7 @@ RENDER_CASES = [
     ("two-perlin-spheres", 40, 24, 4, 50),  # NoiseTexture (Perlin marble), no lights
     ("simple-light", 40, 24, 32, 50),       # + an XY-rect emitter (dark: more samples)
     ("cornell-box-smoke", 32, 32, 4, 50),   # ConstantMedium + Isotropic (free-path draws, stream 2)
+    ("earth", 48, 24, 4, 50),               # ImageTexture: sphere uv (acos, atan2) + texel spectra
 ]
 
 

@@ -143,8 +143,7 @@ def test_random_scene_is_deterministic_per_seed():
     assert any(min(a.textures[i].rgb) < 0 for i in range(a.n_textures))
 
 
-@pytest.mark.parametrize("name,code", [("earth", abi.ERR_UNSUPPORTED), ("next-week-final", abi.ERR_UNSUPPORTED),
-                                       ("nope", abi.ERR_INVALID)])
+@pytest.mark.parametrize("name,code", [("next-week-final", abi.ERR_UNSUPPORTED), ("nope", abi.ERR_INVALID)])
 def test_out_of_scope_presets_fail_loudly(name, code):
     with pytest.raises(yart.YartError) as e:
         yart.Preset(name)

@@ -157,3 +157,48 @@ def test_perlin_presets_draw_two_table_sets():
     assert list(P0.perm_x) != list(P1.perm_x)  # each NoiseTexture::new draws its own tables
     sl = yart.Preset("simple-light").desc.contents
     assert sl.n_objects == 3 and sl.objects[2].kind == abi.PRIM_XY_RECT
+
+
+# ---- ImageTexture (texture.rs:302-345) and get_sphere_uv's acos / atan2 (sphere.rs:213-220)
+def test_acos_atan2_within_one_ulp_of_libm_and_exact_specials():
+    L = O.lib()
+    rng = np.random.default_rng(8)
+    for x in np.concatenate([rng.uniform(-1, 1, 30000), [1.0, -1.0, 0.0, -0.0, 0.5, -0.5, 1e-300]]):
+        got, want = L.oracle_acos(float(x)), math.acos(float(x))
+        assert got == want or abs(got - want) <= math.ulp(want), (x, got, want)
+    ys, xs = rng.normal(size=(2, 30000)) * 10.0 ** rng.uniform(-5, 5, (2, 30000))
+    for y, x in zip(ys, xs):
+        got, want = L.oracle_atan2(float(y), float(x)), math.atan2(float(y), float(x))
+        assert got == want or abs(got - want) <= math.ulp(want), (y, x, got, want)
+    for y, x in [(0.0, 1.0), (-0.0, 1.0), (0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (math.inf, math.inf)]:
+        got, want = L.oracle_atan2(y, x), math.atan2(y, x)
+        assert got == want and math.copysign(1, got) == math.copysign(1, want)
+
+
+def test_image_texture_texel_lookup():
+    b = O.DescBuilder()
+    img = np.random.default_rng(9).integers(0, 256, (8, 16, 3), dtype=np.uint8)
+    t = b.image_texture(img)
+    m = b.material(abi.MAT_LAMBERTIAN, t)
+    b.obj(abi.PRIM_SPHERE, m, (0.0, 0.0, 0.0, 1.0))
+    s = O.OracleScene(b.desc())
+    L = O.lib()
+    p0 = np.zeros(3)
+
+    def want(i, j, wl):
+        rgb = (O.C.c_double * 3)(*[(1.0 / 255.0) * float(c) for c in img[j, i]])
+        return L.oracle_rgb_reflect(rgb, wl)
+
+    # u -> column i = floor(u * W); v is flipped: row j = floor((1 - v) * H); both clamp
+    for u, v, i, j in [(0.0, 1.0, 0, 0), (0.25, 0.75, 4, 2), (0.999, 0.001, 15, 7), (1.0, 0.0, 15, 7),
+                       (1.5, -0.5, 15, 7), (-3.0, 2.0, 0, 0), (math.nan, math.nan, 0, 0)]:
+        assert s.texture(t, 480.0, p0, u, v) == want(i, j, 480.0), (u, v)
+
+
+def test_earth_preset_uses_the_decoded_map():
+    p = yart.Preset("earth")
+    d = p.desc.contents
+    assert d.n_objects == 1 and list(d.objects[0].p[:4]) == [0.0, 0.0, 0.0, 2.0]
+    t = d.textures[d.materials[d.objects[0].material].texture]
+    assert (t.kind, t.width, t.height) == (abi.TEX_IMAGE, 1024, 512)
+    assert list(p.defaults.lookfrom) == [13.0, 2.0, 3.0]

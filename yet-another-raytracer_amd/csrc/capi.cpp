@@ -182,9 +182,17 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     if (textured && m.texture >= d->n_textures) return fail(YART_ERR_INVALID, "texture index out of range");
   }
   for (uint32_t i = 0; i < d->n_textures; ++i) {
-    if (d->textures[i].kind > YART_TEX_NOISE) return fail(YART_ERR_INVALID, "texture kind out of range");
+    if (d->textures[i].kind > YART_TEX_IMAGE) return fail(YART_ERR_INVALID, "texture kind out of range");
     if (d->textures[i].kind == YART_TEX_NOISE && (!d->textures[i].perlin || d->textures[i].noise_type > YART_NOISE_NET))
       return fail(YART_ERR_INVALID, "noise texture without Perlin tables or with a bad noise type");
+  }
+  for (uint32_t i = 0; i < d->n_objects; ++i) {
+    const yart_object& o = d->objects[i];
+    if (o.kind != YART_PRIM_MESH) continue;
+    const yart_material& m = d->materials[o.material];
+    if (m.kind != YART_MAT_NONE && m.kind != YART_MAT_DIELECTRIC && m.texture < d->n_textures &&
+        d->textures[m.texture].kind == YART_TEX_IMAGE)
+      return fail(YART_ERR_UNSUPPORTED, "ImageTexture on a mesh (its texcoords are not uploaded)");
   }
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
@@ -206,6 +214,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     texs[i].kind = t.kind;
     texs[i].noise_type = t.noise_type;
     texs[i].scale = t.scale;
+    texs[i].width = t.kind == YART_TEX_IMAGE && t.pixels ? t.width : 0;
+    texs[i].height = t.kind == YART_TEX_IMAGE && t.pixels ? t.height : 0;
     for (int b = 0; b < kBins; ++b) {
       texs[i].spec[b] = spectrum_bin(t.rgb, b);
       texs[i].spec_even[b] = t.kind == YART_TEX_CHECKER ? spectrum_bin(t.rgb_even, b) : 0.0;
@@ -248,9 +258,13 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   HIP_TRY(upload(s->owned, objs.data(), objs.size(), &ds.objects, bytes), "upload objects");
   HIP_TRY(upload(s->owned, lights.data(), lights.size(), &ds.lights, bytes), "upload lights");
   HIP_TRY(upload(s->owned, mats.data(), mats.size(), &ds.materials, bytes), "upload materials");
-  for (uint32_t i = 0; i < d->n_textures; ++i)
+  for (uint32_t i = 0; i < d->n_textures; ++i) {
     if (d->textures[i].kind == YART_TEX_NOISE)
       HIP_TRY(upload(s->owned, d->textures[i].perlin, 1, &texs[i].perlin, bytes), "upload Perlin tables");
+    if (d->textures[i].kind == YART_TEX_IMAGE && texs[i].width && texs[i].height)
+      HIP_TRY(upload(s->owned, d->textures[i].pixels, (size_t)texs[i].width * texs[i].height * 3, &texs[i].pixels, bytes),
+              "upload image texels");
+  }
   HIP_TRY(upload(s->owned, texs.data(), texs.size(), &ds.textures, bytes), "upload textures");
   HIP_TRY(upload(s->owned, bg, kBins, &ds.background, bytes), "upload background");
   std::vector<DevMesh> dm(d->n_meshes);
@@ -276,7 +290,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   ds.has_ext = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_ext |= d->objects[i].n_xforms && d->objects[i].xforms[0].kind == YART_XF_MEDIUM;
   for (uint32_t i = 0; i < d->n_materials; ++i) ds.has_ext |= d->materials[i].kind == YART_MAT_ISOTROPIC;
-  for (uint32_t i = 0; i < d->n_textures; ++i) ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE;
+  for (uint32_t i = 0; i < d->n_textures; ++i)
+    ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE || d->textures[i].kind == YART_TEX_IMAGE;
 
   yart_scene_info& in = s->info;
   in.device = device; in.n_objects = d->n_objects; in.n_lights = d->n_lights; in.n_meshes = d->n_meshes;

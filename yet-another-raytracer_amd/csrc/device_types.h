@@ -43,6 +43,8 @@ struct DevTexture {
   double spec_even[kBins];  // CHECKER even
   double scale;             // NOISE
   const yart_perlin* perlin;  // NOISE: device copy of the tables
+  uint32_t width, height;   // IMAGE
+  const uint8_t* pixels;    // IMAGE: RGB8 rows, top first (device copy)
 };
 
 struct alignas(16) DevNode {

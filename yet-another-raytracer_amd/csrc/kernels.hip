@@ -54,7 +54,7 @@ __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2])
 struct Ray { V3 o, d; double time, wl; };
 __device__ __forceinline__ V3 at(const Ray& r, double t) { return add(r.o, smul(t, r.d)); }
 
-struct Hit { double t; V3 p, n; bool ff; uint32_t mat; };
+struct Hit { double t; V3 p, n; bool ff; uint32_t mat; double u, v; };  // u, v: EXT kernels only
 
 // ------------------------------------------------- deterministic sin/cos (oracle.c twin)
 __device__ __forceinline__ void rem_pio2(double x, int& q, double& y0, double& y1) {
@@ -149,6 +149,122 @@ __device__ __forceinline__ double log_det(double x) {
   }
   if (k == 0) return f - s * (f - R);
   return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// Deterministic acos / atan2 for get_sphere_uv (sphere.rs:213-220), bitwise oracle_acos /
+// oracle_atan2 (fdlibm __ieee754_acos, atan, __ieee754_atan2).
+__device__ __forceinline__ int32_t hi_word(double x) { return (int32_t)((uint64_t)__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ uint32_t lo_word(double x) { return (uint32_t)(uint64_t)__double_as_longlong(x); }
+__device__ __noinline__ double acos_det(double x) {
+  const double pi = 3.14159265358979311600e+00, pio2_hi = 1.57079632679489655800e+00,
+               pio2_lo = 6.12323399573676603587e-17, pS0 = 1.66666666666666657415e-01,
+               pS1 = -3.25565818622400915405e-01, pS2 = 2.01212532134862925881e-01,
+               pS3 = -4.00555345006794114027e-02, pS4 = 7.91534994289814532176e-04,
+               pS5 = 3.47933107596021167570e-05, qS1 = -2.40339491173441421878e+00,
+               qS2 = 2.02094576023350569471e+00, qS3 = -6.88283971605453293030e-01,
+               qS4 = 7.70381505559019352791e-02;
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff;
+  double z, p, q, r, w, s, c, df;
+  if (ix >= 0x3ff00000) {
+    if (((ix - 0x3ff00000) | (int32_t)lo_word(x)) == 0) return hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3fe00000) {
+    if (ix <= 0x3c600000) return pio2_hi + pio2_lo;
+    z = x * x;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  } else if (hx < 0) {
+    z = (1.0 + x) * 0.5;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    s = sqrt(z);
+    r = p / q;
+    w = r * s - pio2_lo;
+    return pi - 2.0 * (s + w);
+  }
+  z = (1.0 - x) * 0.5;
+  s = sqrt(z);
+  df = __longlong_as_double(__double_as_longlong(s) & (long long)0xffffffff00000000ull);
+  c = (z - df * df) / (s + df);
+  p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  r = p / q;
+  w = r * s + c;
+  return 2.0 * (df + w);
+}
+__device__ __forceinline__ double atan_det(double x) {
+  const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                            1.57079632679489655800e+00};
+  const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                            6.12323399573676603587e-17};
+  const double aT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                         -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                         6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                         -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x44100000) {
+    if (ix > 0x7ff00000 || (ix == 0x7ff00000 && lo_word(x) != 0)) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3fdc0000) {
+    if (ix < 0x3e200000) return x;
+    id = -1;
+  } else {
+    x = fabs(x);
+    if (ix < 0x3ff30000) {
+      if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+      else { id = 1; x = (x - 1.0) / (x + 1.0); }
+    } else {
+      if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+      else { id = 3; x = -1.0 / x; }
+    }
+  }
+  const double z = x * x, w = z * z;
+  const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+  const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+  if (id < 0) return x - x * (s1 + s2);
+  const double zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -zz : zz;
+}
+__device__ __noinline__ double atan2_det(double y, double x) {
+  const double tiny = 1.0e-300, pi_o_4 = 7.8539816339744827900e-01, pi_o_2 = 1.5707963267948965580e+00,
+               pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff, hy = hi_word(y), iy = hy & 0x7fffffff;
+  const uint32_t lx = lo_word(x), ly = lo_word(y);
+  if ((ix | (int32_t)((lx | (0u - lx)) >> 31)) > 0x7ff00000 || (iy | (int32_t)((ly | (0u - ly)) >> 31)) > 0x7ff00000)
+    return x + y;
+  if (((hx - 0x3ff00000) | (int32_t)lx) == 0) return atan_det(y);
+  const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if ((iy | (int32_t)ly) == 0) {
+    if (m <= 1) return y;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if ((ix | (int32_t)lx) == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7ff00000) {
+    if (iy == 0x7ff00000) {
+      if (m == 0) return pi_o_4 + tiny;
+      if (m == 1) return -pi_o_4 - tiny;
+      if (m == 2) return 3.0 * pi_o_4 + tiny;
+      return -3.0 * pi_o_4 - tiny;
+    }
+    if (m == 0) return 0.0;
+    if (m == 1) return -0.0;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if (iy == 0x7ff00000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int k = (iy - ix) >> 20;
+  double z;
+  if (k > 60) z = pi_o_2 + 0.5 * pi_lo;
+  else if (hx < 0 && k < -60) z = 0.0;
+  else z = atan_det(fabs(y / x));
+  if (m == 0) return z;
+  if (m == 1) return -z;
+  if (m == 2) return pi - (z - pi_lo);
+  return (z - pi_lo) - pi;
 }
 
 // ---------------------------------------------------------------- RNG (Philox4x32-10)
@@ -272,6 +388,7 @@ __device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double t
   }
   return true;
 }
+template <bool UV = false>
 __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h) {
   V3 center = mk(p[0], p[1], p[2]);
   double radius = p[3];
@@ -280,6 +397,11 @@ __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double
   if (radius < 0.0) { h.n = neg(outward); h.ff = dot(r.d, outward) > 0.0; }
   else { h.n = outward; h.ff = dot(r.d, outward) < 0.0; }
   h.t = t; h.p = pt;
+  if (UV) {  // get_sphere_uv (sphere.rs:213-220)
+    const double theta = acos_det(-outward.y), phi = atan2_det(-outward.z, outward.x) + kPi;
+    h.u = phi / (2.0 * kPi);
+    h.v = theta / kPi;
+  }
 }
 __device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
   double t;
@@ -303,6 +425,15 @@ __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmi
 }
 // Record of an axis-aligned rect with plane axis `a` (0 yz, 1 xz, 2 xy); a runtime axis lets the
 // rect and box-face records of a wave share one code path.
+// uv (aarect.rs:52-53): the in-plane coordinates b, c computed as in rect_t, over the bounds.
+__device__ __forceinline__ void rect_uv(uint32_t a, const double* bounds, const Ray& r, double t, Hit& h) {
+  const double* o = &r.o.x;
+  const double* d = &r.d.x;
+  const uint32_t B = a == 0 ? 1u : 0u, CC = a == 2 ? 1u : 2u;
+  const double x = o[B] + t * d[B], y = o[CC] + t * d[CC];
+  h.u = (x - bounds[0]) / (bounds[1] - bounds[0]);
+  h.v = (y - bounds[2]) / (bounds[3] - bounds[2]);
+}
 __device__ __forceinline__ void rect_rec(uint32_t a, const Ray& r, double t, Hit& h) {
   V3 outward = mk(a == 0 ? 1.0 : 0.0, a == 1 ? 1.0 : 0.0, a == 2 ? 1.0 : 0.0);
   h.t = t; h.p = at(r, t);
@@ -390,8 +521,13 @@ __device__ __forceinline__ bool triangle_t(const double* p, const Ray& r, double
   if (t < tmin || t > tmax) return false;
   return true;
 }
+template <bool UV = false>
 __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, double t, double u, double v, Hit& h) {
   double w = 1.0 - u - v;
+  if (UV) {  // triangle.rs:93-94
+    h.u = p[18] * w + p[20] * u + p[22] * v;
+    h.v = p[19] * w + p[21] * u + p[23] * v;
+  }
   V3 outward = add(add(muls(ld3(p + 9), w), muls(ld3(p + 12), u)), muls(ld3(p + 15), v));
   h.t = t; h.p = at(r, t);
   if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
@@ -610,18 +746,29 @@ template <bool HAS_MESH, bool EXT>
 __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, const HitId& id, Hit& h) {
   const DevObject& o = S.objects[id.obj];  // per lane
   const uint32_t kind = o.kind, nxf = o.n_xf;
+  if (EXT) { h.u = 0.0; h.v = 0.0; }
   if (EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM) {  // hittable.rs:306-315: at t on the outer ray
     h.t = id.t; h.p = at(r, id.t); h.n = mk(1.0, 0.0, 0.0); h.ff = true; h.mat = o.material;
     return;
   }
   const Ray lr = to_local(o, nxf, r);
   if (kind == YART_PRIM_SPHERE) {
-    sphere_rec(o.p, lr, id.t, h);
+    sphere_rec<EXT>(o.p, lr, id.t, h);
   } else if (kind <= YART_PRIM_BOX) {  // rects and box faces
     const uint32_t a = kind == YART_PRIM_BOX ? 2u - id.sub / 2u : (kind == YART_PRIM_XY_RECT ? 2u : kind == YART_PRIM_XZ_RECT ? 1u : 0u);
     rect_rec(a, lr, id.t, h);
+    if (EXT) {  // the face's rect bounds (box_entity.rs:22-36)
+      const double* p = o.p;
+      double bnd[4] = {p[0], p[1], p[2], p[3]};
+      if (kind == YART_PRIM_BOX) {
+        const uint32_t f = id.sub / 2u;
+        bnd[0] = f == 2 ? p[1] : p[0]; bnd[1] = f == 2 ? p[4] : p[3];
+        bnd[2] = f == 0 ? p[1] : p[2]; bnd[3] = f == 0 ? p[4] : p[5];
+      }
+      rect_uv(a, bnd, lr, id.t, h);
+    }
   } else if (kind == YART_PRIM_TRIANGLE) {
-    triangle_rec(o.p, lr, id.t, id.u, id.v, h);
+    triangle_rec<EXT>(o.p, lr, id.t, id.u, id.v, h);
   } else {
     if constexpr (HAS_MESH) mesh_rec(S.meshes[o.mesh], lr, id.t, id.sub, id.u, id.v, h);
   }
@@ -869,10 +1016,52 @@ __device__ __forceinline__ double perlin_turb(const yart_perlin* P, uint32_t typ
   return fabs(accum);
 }
 
+// Smits basis (color.rs:1711-1982) and RGB::into_spectrum at one bin, as capi.cpp's host copy
+// (texels are reflected at run time: a spectrum per texel would be 150 MB for the earth map).
+__constant__ double c_smits[7][36] = {
+#include "smits.inc"
+};
+__device__ __forceinline__ double rgb_reflect(double red, double green, double blue, int i) {  // color.rs:54-90
+  enum { W, Cy, Ma, Ye, Re, Gr, Bl };
+  double s = 0.0;
+  if (red <= green && red <= blue) {
+    s = red * c_smits[W][i] + s;
+    if (green <= blue) { s = (green - red) * c_smits[Cy][i] + s; s = (blue - green) * c_smits[Bl][i] + s; }
+    else { s = (blue - red) * c_smits[Cy][i] + s; s = (green - blue) * c_smits[Gr][i] + s; }
+  } else if (green <= red && green <= blue) {
+    s = green * c_smits[W][i] + s;
+    if (red <= blue) { s = (red - green) * c_smits[Ma][i] + s; s = (blue - red) * c_smits[Bl][i] + s; }
+    else { s = (blue - green) * c_smits[Ma][i] + s; s = (red - blue) * c_smits[Re][i] + s; }
+  } else {
+    s = blue * c_smits[W][i] + s;
+    if (red <= green) { s = (red - blue) * c_smits[Ye][i] + s; s = (green - red) * c_smits[Gr][i] + s; }
+    else { s = (green - blue) * c_smits[Ye][i] + s; s = (red - green) * c_smits[Re][i] + s; }
+  }
+  return s;
+}
+// f64::clamp (NaN stays NaN) and Rust `f as u32` (saturating, NaN -> 0).
+__device__ __forceinline__ double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+__device__ __forceinline__ uint32_t sat_u32(double f) {
+  if (!(f > 0.0)) return 0u;
+  if (f >= 4294967295.0) return 0xFFFFFFFFu;
+  return (uint32_t)f;
+}
+
 template <bool EXT>
-__device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, double wl, V3 p) {
+__device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, double wl, V3 p, double hu = 0.0,
+                                                double hv = 0.0) {
   const DevTexture& t = S.textures[ti];
   const int bin = spectrum_bin(wl);
+  if (EXT && t.kind == YART_TEX_IMAGE) {  // ImageTexture::value texture.rs:320-344
+    if (!t.pixels || t.width == 0 || t.height == 0) return 1.0;
+    const double uu = clampd(hu, 0.0, 1.0), vv = 1.0 - clampd(hv, 0.0, 1.0);
+    uint32_t i = sat_u32(uu * (double)t.width), j = sat_u32(vv * (double)t.height);
+    if (i >= t.width) i = t.width - 1;
+    if (j >= t.height) j = t.height - 1;
+    const double color_scale = 1.0 / 255.0;
+    const uint8_t* px = t.pixels + (size_t)j * t.width * 3 + (size_t)i * 3;
+    return rgb_reflect(color_scale * (double)px[0], color_scale * (double)px[1], color_scale * (double)px[2], bin);
+  }
   if (EXT && t.kind == YART_TEX_NOISE) {  // NoiseTexture::value texture.rs:265-300 (spec = RGB(1,1,1))
     const double white = t.spec[bin];
     if (t.noise_type == YART_NOISE_NET) return white * perlin_turb(t.perlin, t.noise_type, muls(p, t.scale), 7);
@@ -978,6 +1167,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   bool fresh = !DYN && alive;  // start a sample at the top of the loop
   V3 hp = mk(0.0, 0.0, 0.0), hn = hp;  // the hit to scatter at the top of the next iteration
   uint32_t hmat = 0;
+  double hu = 0.0, hv = 0.0;            // its texture coordinates (EXT)
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
 
   while (alive) {
@@ -1038,7 +1228,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       const DevMaterial& m = S.materials[hmat];
       const uint32_t kind = m.kind;
       if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
         const Onb uvw = onb_from_w(hn);
         V3 dir;
         double pdf_val;
@@ -1071,7 +1261,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           depth--;
         }
       } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
         V3 p;
         for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
           const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
@@ -1090,7 +1280,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           p = mk(px, py, pz);
           if (!(len2(p) >= 1.0)) break;
         }
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp);
+        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
         T = T * att;
         ray.o = hp;
         ray.d = add(reflected, smul(m.fuzz, p));
@@ -1152,9 +1342,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC ||
               (EXT && kind == YART_MAT_ISOTROPIC)) {
             hp = h.p; hn = h.n; hmat = h.mat;  // scattered at the top of the next iteration
+            if (EXT) { hu = h.u; hv = h.v; }
           } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
             double emitted = 0.0;
-            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, ray.wl, h.p);
+            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, ray.wl, h.p, h.u, h.v);
             R = T * emitted;
             term = true;
           }
@@ -1288,6 +1479,8 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
     case 2: sincos_det(a[i], s, c); out[i] = s; break;
     case 3: sincos_det(a[i], s, c); out[i] = c; break;
     case 5: out[i] = log_det(a[i]); break;
+    case 6: out[i] = acos_det(a[i]); break;
+    case 7: out[i] = atan2_det(a[i], b[i]); break;
     default: out[i] = pow(a[i], b[i]); break;
   }
 }

@@ -33,7 +33,8 @@ const Material SF66 = Dielectric(2.0245976, 0.470187196, 2.59970433, 0.014705322
 // ------------------------------------------------------------------------ flattening
 static bool same_texture(const yart_texture& a, const Texture& t) {
   return a.kind == t.kind && !std::memcmp(a.rgb, t.a.e, sizeof a.rgb) && !std::memcmp(a.rgb_even, t.b.e, sizeof a.rgb_even) &&
-         a.noise_type == t.noise_type && a.scale == t.scale && a.perlin == t.perlin.get();
+         a.noise_type == t.noise_type && a.scale == t.scale && a.perlin == t.perlin.get() &&
+         a.pixels == (t.pixels ? t.pixels->data() : nullptr);
 }
 uint32_t Flattener::texture(const Texture& t) {
   for (size_t i = 0; i < out_.textures.size(); ++i)
@@ -47,6 +48,12 @@ uint32_t Flattener::texture(const Texture& t) {
   if (t.perlin) {
     out_.perlins.push_back(t.perlin);
     y.perlin = t.perlin.get();
+  }
+  if (t.pixels) {
+    out_.images.push_back(t.pixels);
+    y.pixels = t.pixels->data();
+    y.width = t.width;
+    y.height = t.height;
   }
   out_.textures.push_back(y);
   return (uint32_t)(out_.textures.size() - 1);
@@ -151,6 +158,33 @@ void ConstantMedium::flatten(Flattener& f, std::vector<yart_xform>& chain) const
   f.override_material(nullptr);
   chain.pop_back();
   if (n != 1) throw std::runtime_error("a ConstantMedium boundary must be one primitive");
+}
+
+Texture ImageTexture(const std::string& ppm_path) {
+  std::ifstream in(ppm_path, std::ios::binary);
+  if (!in) throw std::runtime_error("cannot open image " + ppm_path + " (decode it with tools/decode_image.py)");
+  auto token = [&in]() {
+    std::string t;
+    char c;
+    while (in.get(c)) {
+      if (c == '#') { std::string skip; std::getline(in, skip); continue; }
+      if (std::isspace((unsigned char)c)) { if (!t.empty()) break; continue; }
+      t.push_back(c);
+    }
+    return t;
+  };
+  if (token() != "P6") throw std::runtime_error(ppm_path + ": not a binary PPM (P6)");
+  const long w = std::stol(token()), h = std::stol(token()), maxv = std::stol(token());
+  if (w <= 0 || h <= 0 || maxv != 255) throw std::runtime_error(ppm_path + ": unsupported PPM header");
+  auto px = std::make_shared<std::vector<uint8_t>>((size_t)w * (size_t)h * 3);
+  if (!in.read(reinterpret_cast<char*>(px->data()), (std::streamsize)px->size()))
+    throw std::runtime_error(ppm_path + ": truncated PPM");
+  Texture t;
+  t.kind = YART_TEX_IMAGE;
+  t.width = (uint32_t)w;
+  t.height = (uint32_t)h;
+  t.pixels = px;
+  return t;
 }
 
 Texture NoiseTexture(uint32_t noise_type, double scale, SceneRng& rng) {

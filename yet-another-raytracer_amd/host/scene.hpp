@@ -39,12 +39,17 @@ struct Texture {
   uint32_t noise_type = 0;
   double scale = 0.0;
   std::shared_ptr<const yart_perlin> perlin;  // NOISE: its own tables (Perlin::new per texture)
+  uint32_t width = 0, height = 0;              // IMAGE
+  std::shared_ptr<const std::vector<uint8_t>> pixels;  // IMAGE: RGB8 rows, top first
 };
 inline Texture SolidColor(RGB c) { Texture t; t.kind = YART_TEX_SOLID; t.a = c; return t; }       // texture.rs:18-40
 inline Texture CheckerTexture(RGB odd, RGB even) { Texture t; t.kind = YART_TEX_CHECKER; t.a = odd; t.b = even; return t; }  // texture.rs:42-68
 // NoiseTexture::new (texture.rs:251-260): Perlin::new draws its tables from thread_rng in the
 // reference; here from the scene's seeded stream, in the same order (ranfloat, ranvec, perm_x/y/z).
 Texture NoiseTexture(uint32_t noise_type, double scale, SceneRng& rng);
+// ImageTexture::new (texture.rs:302-318) over a binary PPM (P6) holding the decoded texels of the
+// image the reference opens (tools/decode_image.py). Throws std::runtime_error.
+Texture ImageTexture(const std::string& ppm_path);
 
 // ----------------------------------------------------------------- materials (material.rs)
 struct Material {
@@ -179,6 +184,7 @@ class SceneDesc {
   std::vector<yart_texture> textures;
   std::vector<std::shared_ptr<const MeshData>> mesh_data;
   std::vector<std::shared_ptr<const yart_perlin>> perlins;  // tables the noise textures point at
+  std::vector<std::shared_ptr<const std::vector<uint8_t>>> images;  // texels the image textures point at
   std::vector<yart_mesh> meshes;
   double background[3] = {0, 0, 0};
   yart_scene_desc desc() const;

@@ -5,7 +5,7 @@ ABI_VERSION = 1
 
 OK, ERR_INVALID, ERR_DEVICE, ERR_NO_MEMORY, ERR_UNSUPPORTED, ERR_IO = 0, -1, -2, -3, -4, -5
 
-TEX_SOLID, TEX_CHECKER, TEX_NOISE = 0, 1, 2
+TEX_SOLID, TEX_CHECKER, TEX_NOISE, TEX_IMAGE = 0, 1, 2, 3
 NOISE_SQUARE, NOISE_TRILINEAR, NOISE_SMOOTH, NOISE_MARBLE, NOISE_NET = range(5)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC = 0, 1, 2, 3, 4, 5
 PRIM_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT, PRIM_BOX, PRIM_TRIANGLE, PRIM_MESH = range(7)
@@ -22,7 +22,8 @@ class Perlin(C.Structure):
 
 class Texture(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("noise_type", C.c_uint32), ("rgb", D3), ("rgb_even", D3), ("scale", C.c_double),
-                ("perlin", C.POINTER(Perlin))]
+                ("perlin", C.POINTER(Perlin)), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("pixels", C.POINTER(C.c_uint8))]
 
 
 class Material(C.Structure):
