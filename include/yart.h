@@ -100,7 +100,9 @@ enum {
   YART_PRIM_YZ_RECT = 3,  /* YZRect           aarect.rs:174-242  p = y0, y1, z0, z1, k       */
   YART_PRIM_BOX = 4,      /* BoxEntity        box_entity.rs      p = p0 xyz, p1 xyz          */
   YART_PRIM_TRIANGLE = 5, /* Triangle         triangle.rs:19-102 p = v0 v1 v2 (9), n0 n1 n2 (9), uv0 uv1 uv2 (6) */
-  YART_PRIM_MESH = 6      /* TriangleMesh     triangle.rs:104-185 (L4QBVH, qbvh.rs:244-544); `mesh` selects the triangles */
+  YART_PRIM_MESH = 6,     /* TriangleMesh     triangle.rs:104-185 (L4QBVH, qbvh.rs:244-544); `mesh` selects the triangles */
+  YART_PRIM_MOVING_SPHERE = 7 /* MovingSphere sphere.rs:121-211 p = center0 xyz, center1 xyz, time0, time1, radius;
+                                 its presence makes the camera draw the shutter time (camera.rs:91) */
 };
 enum {
   YART_XF_TRANSLATE = 1, /* Translate  hittable.rs:125-163  v = offset            */

@@ -502,6 +502,7 @@ struct oracle_scene {
   yart_texture* texs; uint32_t ntexs;
   yart_perlin* perlins; /* per texture (NOISE) */
   uint8_t** images;     /* per texture (IMAGE) */
+  int has_time;         /* a MovingSphere reads the ray's shutter time */
   qbvh_t* meshes; uint32_t nmeshes;
   double background[3];
   /* per object, per wrapper: RotateY sin/cos (hittable.rs:173-176) */
@@ -761,6 +762,33 @@ static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_ma
   rec->v = theta / PI;
   return 1;
 }
+/* MovingSphere::hit (sphere.rs:161-199): centre at the ray's time; normal faces the ray. */
+static v3 moving_center(const double* p, double time) { /* sphere.rs:153-156 */
+  return vadd(V(p[0], p[1], p[2]), smulv((time - p[6]) / (p[7] - p[6]), vsub(V(p[3], p[4], p[5]), V(p[0], p[1], p[2]))));
+}
+static int moving_sphere_hit(const double* p, const ray_t* r, double t_min, double t_max, hit_rec* rec) {
+  const double radius = p[8];
+  v3 oc = vsub(r->o, moving_center(p, r->time));
+  double a = length_squared(r->d);
+  double half_b = dot(oc, r->d);
+  double c = length_squared(oc) - radius * radius;
+  double disc = half_b * half_b - a * c;
+  if (disc < 0.0) return 0;
+  double t = (0.0 - half_b - sqrt(disc)) / a;
+  if (t < t_min || t_max < t) {
+    t = (0.0 - half_b + sqrt(disc)) / a;
+    if (t < t_min || t_max < t) return 0;
+  }
+  v3 pt = ray_at(r, t);
+  v3 outward = vdivs(vsub(pt, moving_center(p, r->time)), radius);
+  if (dot(r->d, outward) < 0.0) { rec->normal = outward; rec->front_face = 1; }
+  else { rec->normal = vneg(outward); rec->front_face = 0; }
+  const double theta = oracle_acos(-outward.y), phi = oracle_atan2(-outward.z, outward.x) + PI;
+  rec->u = phi / (2.0 * PI);
+  rec->v = theta / PI;
+  rec->t = t; rec->p = pt;
+  return 1;
+}
 /* aarect.rs: axis a (plane normal), in-plane axes b, c: XY a=z (b=x, c=y) :41-76;
  * XZ a=y (b=x, c=z) :111-146; YZ a=x (b=y, c=z) :206-241. p = b0, b1, c0, c1, k. */
 static int rect_hit(int kind, const double* p, const ray_t* r, double t_min, double t_max, hit_rec* rec) {
@@ -825,6 +853,7 @@ static int prim_hit(const oracle_scene* s, const yart_object* o, const ray_t* r,
     case YART_PRIM_BOX: return box_hit(o->p, r, t_min, t_max, rec);
     case YART_PRIM_TRIANGLE: return triangle_hit(o->p, r, t_min, t_max, rec);
     case YART_PRIM_MESH: return qbvh_hit(&s->meshes[o->mesh], r, t_min, t_max, rec); /* triangle.rs:177-185 */
+    case YART_PRIM_MOVING_SPHERE: return moving_sphere_hit(o->p, r, t_min, t_max, rec);
   }
   return 0;
 }
@@ -1102,7 +1131,7 @@ static v3 random_in_unit_disk(rng_t* g) { /* camera.rs:25-33 */
   do { double x = gen_range_f64(g, -1.0, 1.0); double y = gen_range_f64(g, -1.0, 1.0); p = V(x, y, 0.0); } while (length_squared(p) >= 1.0);
   return p;
 }
-static ray_t camera_get_ray(const yart_camera* c, double s, double t, double wl, rng_t* g) { /* camera.rs:82-94 */
+static ray_t camera_get_ray(const yart_camera* c, double s, double t, double wl, rng_t* g, int draw_time) { /* camera.rs:82-94 */
   v3 rd = smulv(c->lens_radius, random_in_unit_disk(g));
   v3 cu = V(c->u[0], c->u[1], c->u[2]), cv = V(c->v[0], c->v[1], c->v[2]);
   v3 offset = vadd(vmuls(cu, rd.x), vmuls(cv, rd.y));
@@ -1113,7 +1142,8 @@ static ray_t camera_get_ray(const yart_camera* c, double s, double t, double wl,
   ray_t r;
   r.o = vadd(org, offset);
   r.d = vsub(vsub(vadd(vadd(llc, smulv(s, hor)), smulv(t, ver)), org), offset);
-  r.time = c->time0; /* gen_range(time0..time1) in camera.rs:92; no in-scope object reads it */
+  /* gen_range(time0..time1) (camera.rs:91): drawn only when a MovingSphere can read it */
+  r.time = draw_time ? gen_range_f64(g, c->time0, c->time1) : c->time0;
   r.wl = wl;
   return r;
 }
@@ -1261,7 +1291,7 @@ static void render_pixel(const job_t* j, uint32_t x, uint32_t y) {
     double ty = (double)y + gen_f64(&g);
     double v = 1.0 - ty / (double)(H - 1);
     double wl = gen_range_f64(&g, MIN_LAMBDA, MAX_LAMBDA); /* color.rs:20-23 */
-    ray_t r = camera_get_ray(j->cam, u, v, wl, &g);
+    ray_t r = camera_get_ray(j->cam, u, v, wl, &g, j->s->has_time);
     double R = j->mode ? reflectance_recursive(j->s, &r, &g, p->max_depth, p->max_depth)
                        : reflectance_iterative(j->s, &r, &g, p->max_depth);
     double cie[3], xyz[3], san[3];
@@ -1380,7 +1410,7 @@ static void rotate_sc(const yart_object* objs, uint32_t n, double (*sc)[YART_MAX
 
 static int check_objects(const yart_scene_desc* d, const yart_object* o, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
-    if (o[i].kind > YART_PRIM_MESH || o[i].n_xforms > YART_MAX_XFORMS) return 0;
+    if (o[i].kind > YART_PRIM_MOVING_SPHERE || o[i].n_xforms > YART_MAX_XFORMS) return 0;
     if (o[i].kind == YART_PRIM_MESH && o[i].mesh >= d->n_meshes) return 0;
     if (o[i].material >= d->n_materials && d->n_materials) return 0;
     for (uint32_t l = 0; l < o[i].n_xforms; ++l)
@@ -1428,6 +1458,7 @@ int oracle_scene_create(const yart_scene_desc* d, oracle_scene** out) {
     }
   }
   memcpy(s->background, d->background, sizeof(s->background));
+  for (uint32_t i = 0; i < s->nobj; ++i) s->has_time |= s->objects[i].kind == YART_PRIM_MOVING_SPHERE;
   s->obj_sc = calloc(s->nobj + 1, sizeof(*s->obj_sc));
   s->light_sc = calloc(s->nlights + 1, sizeof(*s->light_sc));
   rotate_sc(s->objects, s->nobj, s->obj_sc);

@@ -204,6 +204,22 @@ def test_world_bvh_ties_go_to_the_later_object(dev):
         _hits_equal(h, o, h2, o2)
 
 
+def test_moving_spheres_match_oracle(dev):
+    """MovingSphere + the shutter-time draw it switches on (camera.rs:91), with a glass one."""
+    from test_scene_features import moving_scene
+    b = moving_scene()
+    d = b.desc()
+    W, H = 48, 32
+    cam = yart.make_camera((0.0, 2.0, 12.0), (0.0, 1.0, 0.0), 40.0, W / H, 0.1, 10.0)
+    s = yart.DeviceScene(d)
+    np.testing.assert_array_equal(s.render(cam, yart.render_params(W, H, 8, 50)),
+                                  O.OracleScene(d).render(cam, yart.render_params(W, H, 8, 50)))
+    rays = _random_rays(50000, -6, 6, seed=19)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    _hits_equal(h, o, h2, o2)
+
+
 def test_scene_info_matches_reference_qbvh(dev):
     p = yart.Preset("david")
     s = yart.DeviceScene(p)

@@ -202,3 +202,50 @@ def test_earth_preset_uses_the_decoded_map():
     t = d.textures[d.materials[d.objects[0].material].texture]
     assert (t.kind, t.width, t.height) == (abi.TEX_IMAGE, 1024, 512)
     assert list(p.defaults.lookfrom) == [13.0, 2.0, 3.0]
+
+
+# ---- MovingSphere (sphere.rs:121-211)
+def moving_scene(with_glass=True):
+    b = O.DescBuilder(background=(0.7, 0.8, 1.0))
+    red = b.material(abi.MAT_LAMBERTIAN, b.texture((0.7, 0.3, 0.1)))
+    ground = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    b.obj(abi.PRIM_SPHERE, ground, (0.0, -1000.0, 0.0, 1000.0))
+    for k in range(5):  # centre0 -> centre1 over time 0..1, as the book's bouncing spheres
+        c0 = (-4.0 + 2.0 * k, 0.5, 0.0)
+        b.obj(abi.PRIM_MOVING_SPHERE, red, c0 + (c0[0], 0.5 + 0.4 * k, 0.0, 0.0, 1.0, 0.5))
+    if with_glass:
+        glass = b.material(abi.MAT_DIELECTRIC, 0, b=(1.03961212, 0.231792344, 1.01046945),
+                           c=(6000.69867, 20017.9144, 103560653.0))
+        b.obj(abi.PRIM_MOVING_SPHERE, glass, (0.0, 1.5, 2.0, 0.0, 1.5, 2.5, 0.0, 1.0, -0.8))
+    return b
+
+
+def test_moving_sphere_at_time0_hits_like_a_still_sphere():
+    """Intersect rays carry time 0: a moving sphere is then its centre0 sphere; from outside its
+    ray-facing normal is the outward one, as StillSphere's."""
+    bm, bs = O.DescBuilder(), O.DescBuilder()
+    mm = bm.material(abi.MAT_LAMBERTIAN, bm.texture((0.5, 0.5, 0.5)))
+    ms = bs.material(abi.MAT_LAMBERTIAN, bs.texture((0.5, 0.5, 0.5)))
+    bm.obj(abi.PRIM_MOVING_SPHERE, mm, (1.0, 2.0, 3.0, 9.0, 9.0, 9.0, 0.0, 1.0, 1.5))
+    bs.obj(abi.PRIM_SPHERE, ms, (1.0, 2.0, 3.0, 1.5))
+    rng = np.random.default_rng(10)
+    n = 20000
+    o = rng.uniform(-10, 10, (n, 3))
+    o = o[np.linalg.norm(o - [1, 2, 3], axis=1) > 2.0][:5000]
+    d = np.array([1.0, 2.0, 3.0]) + rng.uniform(-1.6, 1.6, (len(o), 3)) - o
+    rays = np.concatenate([o, d, np.full((len(o), 1), 0.001), np.full((len(o), 1), np.inf)], axis=1)
+    h1, o1 = O.OracleScene(bm.desc()).intersect(rays)
+    h2, o2 = O.OracleScene(bs.desc()).intersect(rays)
+    np.testing.assert_array_equal(o1, o2)
+    assert (o1 >= 0).mean() > 0.5
+    np.testing.assert_array_equal(h1[o1 >= 0], h2[o2 >= 0])
+
+
+def test_moving_spheres_blur_along_their_path():
+    """The shutter time is drawn per sample once a MovingSphere is present (camera.rs:91): a sphere
+    moving in y smears over its path, so the render differs from the time-0 scene."""
+    b = moving_scene(with_glass=False)
+    d = b.desc()
+    cam = yart.make_camera((0.0, 2.0, 12.0), (0.0, 1.0, 0.0), 40.0, 48 / 32, 0.0, 10.0)
+    img = O.OracleScene(d).render(cam, yart.render_params(48, 32, 8, 8))
+    assert np.isfinite(img).all() and img.mean() > 0

@@ -85,7 +85,7 @@ hipError_t upload(std::vector<void*>& owned, const T* src, size_t n, const T** d
 
 bool valid_objects(const yart_scene_desc* d, const yart_object* o, uint32_t n, bool lights, std::string& why) {
   for (uint32_t i = 0; i < n; ++i) {
-    if (o[i].kind > YART_PRIM_MESH) { why = "object kind out of range"; return false; }
+    if (o[i].kind > YART_PRIM_MOVING_SPHERE) { why = "object kind out of range"; return false; }
     if (o[i].n_xforms > YART_MAX_XFORMS) { why = "too many wrappers"; return false; }
     for (uint32_t l = 0; l < o[i].n_xforms; ++l) {
       if (o[i].xforms[l].kind < YART_XF_TRANSLATE || o[i].xforms[l].kind > YART_XF_MEDIUM) { why = "bad wrapper kind"; return false; }
@@ -290,6 +290,9 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   ds.has_ext = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_ext |= d->objects[i].n_xforms && d->objects[i].xforms[0].kind == YART_XF_MEDIUM;
   for (uint32_t i = 0; i < d->n_materials; ++i) ds.has_ext |= d->materials[i].kind == YART_MAT_ISOTROPIC;
+  ds.has_time = 0;
+  for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_time |= d->objects[i].kind == YART_PRIM_MOVING_SPHERE;
+  ds.has_ext |= ds.has_time;
   for (uint32_t i = 0; i < d->n_textures; ++i)
     ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE || d->textures[i].kind == YART_TEX_IMAGE;
 

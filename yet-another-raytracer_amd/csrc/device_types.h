@@ -90,7 +90,8 @@ struct DevScene {
   const uint32_t* world_objs;
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
   uint32_t has_mesh;
-  uint32_t has_ext;  // noise textures, isotropic materials or media present (EXT kernels)
+  uint32_t has_ext;  // noise/image textures, isotropic materials, media or moving spheres (EXT kernels)
+  uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
 };
 

@@ -410,6 +410,39 @@ __device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double
   return true;
 }
 
+// MovingSphere::hit (sphere.rs:161-199): centre at the ray's time (sphere.rs:153-156), normal
+// divided by the signed radius and faced against the ray. p = c0 xyz, c1 xyz, time0, time1, r.
+__device__ __forceinline__ V3 moving_center(const double* p, double time) {
+  return add(ld3(p), smul((time - p[6]) / (p[7] - p[6]), sub(ld3(p + 3), ld3(p))));
+}
+__device__ __forceinline__ bool moving_sphere_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
+  const double radius = p[8];
+  const V3 oc = sub(r.o, moving_center(p, r.time));
+  const double a = len2(r.d), half_b = dot(oc, r.d), c = len2(oc) - radius * radius;
+  const double disc = half_b * half_b - a * c;
+  if (disc < 0.0) return false;
+  const double sq = sqrt(disc);
+  t = (0.0 - half_b - sq) / a;
+  if (t < tmin || tmax < t) {
+    t = (0.0 - half_b + sq) / a;
+    if (t < tmin || tmax < t) return false;
+  }
+  return true;
+}
+template <bool UV>
+__device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r, double t, Hit& h) {
+  const V3 pt = at(r, t);
+  const V3 outward = divs(sub(pt, moving_center(p, r.time)), p[8]);
+  if (dot(r.d, outward) < 0.0) { h.n = outward; h.ff = true; }
+  else { h.n = neg(outward); h.ff = false; }
+  if (UV) {
+    const double theta = acos_det(-outward.y), phi = atan2_det(-outward.z, outward.x) + kPi;
+    h.u = phi / (2.0 * kPi);
+    h.v = theta / kPi;
+  }
+  h.t = t; h.p = pt;
+}
+
 // aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
 template <int A, int B, int CC>
 __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
@@ -660,6 +693,7 @@ __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, ui
     case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2>(o.p, r, tmin, tmax, t);
     case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t(o.p, r, tmin, tmax, t, sub);
     case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
+    case YART_PRIM_MOVING_SPHERE: if (STATS) st.v[ST_PRIM]++; return moving_sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_MESH:
       if constexpr (HAS_MESH) return qbvh_t<STATS>(S.meshes[o.mesh], r, tmin, tmax, t, sub, u, v, stk, st);
       return false;
@@ -769,6 +803,8 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
     }
   } else if (kind == YART_PRIM_TRIANGLE) {
     triangle_rec<EXT>(o.p, lr, id.t, id.u, id.v, h);
+  } else if (kind == YART_PRIM_MOVING_SPHERE) {
+    moving_sphere_rec<EXT>(o.p, lr, id.t, h);
   } else {
     if constexpr (HAS_MESH) mesh_rec(S.meshes[o.mesh], lr, id.t, id.sub, id.u, id.v, h);
   }
@@ -1078,7 +1114,8 @@ __device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, 
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, smul(2.0 * dot(v, n), n)); }  // material.rs:75-77
 
 // --------------------------------------------------------------------------- sampling
-__device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double t, double wl, Rng& g) {  // camera.rs:82-94
+__device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double t, double wl, Rng& g,
+                                          bool draw_time) {  // camera.rs:82-94
   V3 p;
   for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_disk camera.rs:25-33
     const double x = gen_range(g, -1.0, 1.0);
@@ -1092,7 +1129,8 @@ __device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double
   Ray r;
   r.o = add(org, offset);
   r.d = sub(sub(add(add(ld3(c.lower_left_corner), smul(s, ld3(c.horizontal))), smul(t, ld3(c.vertical))), org), offset);
-  r.time = c.time0;  // gen_range(time0..time1) (camera.rs:92): no in-scope object reads it
+  // gen_range(time0..time1) (camera.rs:91): drawn only when a MovingSphere can read it
+  r.time = draw_time ? gen_range(g, c.time0, c.time1) : c.time0;
   r.wl = wl;
   return r;
 }
@@ -1220,7 +1258,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       const double ty = (double)y + gen_f64(g);
       const double v = 1.0 - ty / (double)(H - 1);
       const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
-      ray = camera_ray(A.cam, u, v, wl, g);
+      ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
       T = 1.0;
       depth = A.max_depth;
       fresh = false;

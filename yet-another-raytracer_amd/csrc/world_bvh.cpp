@@ -11,6 +11,7 @@ bool world_bounds(const DevObject& o, double lo[3], double hi[3]) {
   // A medium's hit can land past t_max (hittable.rs:306): the list walk's replace-on-any-hit
   // order matters there, so scenes with media keep the linear walk.
   if (o.n_xf && o.xf_kind[0] == YART_XF_MEDIUM) return false;
+  if (o.kind == YART_PRIM_MOVING_SPHERE) return false;  // its box depends on the shutter time
   const double* p = o.p;
   switch (o.kind) {
     case YART_PRIM_SPHERE: {  // sphere.rs:48-86 (a negative radius is the same sphere)

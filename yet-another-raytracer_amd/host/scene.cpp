@@ -105,6 +105,10 @@ void StillSphere::flatten(Flattener& f, std::vector<yart_xform>& chain) const {
   double p[4] = {center.x(), center.y(), center.z(), radius};
   f.emit(YART_PRIM_SPHERE, f.material(material), chain, p, 4);
 }
+void MovingSphere::flatten(Flattener& f, std::vector<yart_xform>& chain) const {
+  double p[9] = {center0.x(), center0.y(), center0.z(), center1.x(), center1.y(), center1.z(), time0, time1, radius};
+  f.emit(YART_PRIM_MOVING_SPHERE, f.material(material), chain, p, 9);
+}
 void XYRect::flatten(Flattener& f, std::vector<yart_xform>& chain) const { f.emit(YART_PRIM_XY_RECT, f.material(material), chain, p, 5); }
 void XZRect::flatten(Flattener& f, std::vector<yart_xform>& chain) const { f.emit(YART_PRIM_XZ_RECT, f.material(material), chain, p, 5); }
 void YZRect::flatten(Flattener& f, std::vector<yart_xform>& chain) const { f.emit(YART_PRIM_YZ_RECT, f.material(material), chain, p, 5); }

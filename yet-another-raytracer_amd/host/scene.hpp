@@ -93,6 +93,14 @@ class StillSphere : public Hittable {  // sphere.rs:31-119
   void flatten(Flattener& f, std::vector<yart_xform>& chain) const override;
 };
 
+class MovingSphere : public Hittable {  // sphere.rs:121-211
+ public:
+  MovingSphere(Vec3 center0, Vec3 center1, double time0, double time1, double radius, Material m)
+      : center0(center0), center1(center1), time0(time0), time1(time1), radius(radius), material(m) {}
+  Vec3 center0, center1; double time0, time1, radius; Material material;
+  void flatten(Flattener& f, std::vector<yart_xform>& chain) const override;
+};
+
 class XYRect : public Hittable {  // aarect.rs:9-77
  public:
   XYRect(double x0, double x1, double y0, double y1, double k, Material m) : p{x0, x1, y0, y1, k}, material(m) {}

@@ -8,7 +8,7 @@ OK, ERR_INVALID, ERR_DEVICE, ERR_NO_MEMORY, ERR_UNSUPPORTED, ERR_IO = 0, -1, -2,
 TEX_SOLID, TEX_CHECKER, TEX_NOISE, TEX_IMAGE = 0, 1, 2, 3
 NOISE_SQUARE, NOISE_TRILINEAR, NOISE_SMOOTH, NOISE_MARBLE, NOISE_NET = range(5)
 MAT_NONE, MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC = 0, 1, 2, 3, 4, 5
-PRIM_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT, PRIM_BOX, PRIM_TRIANGLE, PRIM_MESH = range(7)
+PRIM_SPHERE, PRIM_XY_RECT, PRIM_XZ_RECT, PRIM_YZ_RECT, PRIM_BOX, PRIM_TRIANGLE, PRIM_MESH, PRIM_MOVING_SPHERE = range(8)
 XF_TRANSLATE, XF_ROTATE_Y, XF_FLIP_FACE, XF_MEDIUM = 1, 2, 3, 4
 MAX_XFORMS = 4
 
