@@ -321,7 +321,7 @@ static inline double powi5(double x) { double x2 = x * x; return x * (x2 * x2); 
  * rand::thread_rng, whose stream is not reproducible, so the stream layout is this
  * implementation's own; phases let the GPU compute each bounce's blocks at one place in its
  * loop. Draws whose value cannot reach any output are not taken (a one-element index range,
- * the ray time no in-scope object reads). The mappings from u64 to the values the reference
+ * the ray time when no MovingSphere reads it). The mappings from u64 to the values the reference
  * asks rand 0.8.5 for are restated below. */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
