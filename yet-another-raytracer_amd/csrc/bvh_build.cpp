@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 namespace yart_dev {
@@ -51,13 +52,15 @@ struct Builder {
   Result leaf(uint32_t off, uint32_t n, const double* normals) {
     Box b = tri_box[perm[off]];
     for (uint32_t i = 1; i < n; ++i) b = merge(b, tri_box[perm[off + i]]);
-    uint32_t li = (uint32_t)out->leaf_first.size();
-    out->leaf_first.push_back(off);
+    uint32_t li = (uint32_t)(out->leaves.size() / kLeafFloats);
     size_t base = out->leaves.size();
-    out->leaves.resize(base + 36, 0.0f);
+    out->leaves.resize(base + kLeafFloats, 0.0f);
     for (uint32_t i = 0; i < n; ++i) {
       const float* v = &pos[9 * (size_t)perm[off + i]];
-      for (int c = 0; c < 9; ++c) out->leaves[base + 4 * c + i] = v[c];
+      float* rec = &out->leaves[base + 12 * i];
+      for (int c = 0; c < 9; ++c) rec[c] = v[c];
+      const uint32_t tri = off + i;  // sorted index: the row of the normal table
+      std::memcpy(&rec[9], &tri, 4);
       const double* nn = &normals[9 * (size_t)perm[off + i]];
       for (int c = 0; c < 9; ++c) out->normals[9 * (size_t)(off + i) + c] = nn[c];
     }
@@ -78,15 +81,19 @@ struct Builder {
     Result rr = construct(off + nl + nr / 2, nr - nr / 2, level + 1, normals);
     DevNode node{};
     const Result* ch[4] = {&ll, &lr, &rl, &rr};
+    const uint32_t axes = (uint32_t)top | ((uint32_t)la << 2) | ((uint32_t)ra << 4);
     for (int k = 0; k < 4; ++k) {
+      // QBVHNode::new fills empty lanes with f64::MAX (qbvh.rs:570-572); +inf misses the same way.
+      float mn[3], mx[3];
       for (int a = 0; a < 3; ++a) {
-        // QBVHNode::new fills empty lanes with f64::MAX (qbvh.rs:570-572); +inf misses the same way.
-        node.bmin[a][k] = ch[k]->has ? (float)ch[k]->box.mn[a] : INFINITY;
-        node.bmax[a][k] = ch[k]->has ? (float)ch[k]->box.mx[a] : INFINITY;
+        mn[a] = ch[k]->has ? (float)ch[k]->box.mn[a] : INFINITY;
+        mx[a] = ch[k]->has ? (float)ch[k]->box.mx[a] : INFINITY;
       }
-      node.child[k] = ch[k]->id;
+      node.lo[k][0] = mn[0]; node.lo[k][1] = mn[1]; node.lo[k][2] = mn[2]; node.lo[k][3] = mx[0];
+      node.hi[k][0] = mx[1]; node.hi[k][1] = mx[2];
+      std::memcpy(&node.hi[k][2], &ch[k]->id, 4);
+      std::memcpy(&node.hi[k][3], &axes, 4);
     }
-    node.axes = (uint32_t)top | ((uint32_t)la << 2) | ((uint32_t)ra << 4);
     out->nodes.push_back(node);
     Box lb = ll.has && lr.has ? merge(ll.box, lr.box) : (ll.has ? ll.box : lr.box);
     Box rb = rl.has && rr.has ? merge(rl.box, rr.box) : (rl.has ? rl.box : rr.box);

@@ -10,8 +10,7 @@ namespace yart_dev {
 
 struct BuiltMesh {
   std::vector<DevNode> nodes;       // post-order; root = nodes.back()
-  std::vector<float> leaves;        // 36 floats per leaf (SoA, see DevMesh)
-  std::vector<uint32_t> leaf_first; // first sorted triangle of each leaf
+  std::vector<float> leaves;        // kLeafFloats per leaf (see DevNode)
   std::vector<double> normals;      // 9 per sorted triangle
   uint32_t depth = 0;               // inner-node levels on the deepest path
 };

@@ -231,7 +231,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     std::string err;
     if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err)) return fail(YART_ERR_UNSUPPORTED, err);
     nodes += (uint32_t)built[m].nodes.size();
-    leaves += (uint32_t)built[m].leaf_first.size();
+    leaves += (uint32_t)(built[m].leaves.size() / kLeafFloats);
     depth = std::max(depth, built[m].depth);
   }
 
@@ -272,7 +272,6 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     BuiltMesh& b = built[m];
     HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
     HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
-    HIP_TRY(upload(s->owned, b.leaf_first.data(), b.leaf_first.size(), &dm[m].leaf_first, bytes), "upload leaf_first");
     HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
     dm[m].root = (uint32_t)b.nodes.size() - 1;
     dm[m].n_nodes = (uint32_t)b.nodes.size();

@@ -8,8 +8,8 @@
 //              reference recomputes the whole spectrum per lookup and reads one bin; the bins are
 //              bitwise the values it would read.
 //  Mesh BLAS   the reference's L4QBVH (qbvh.rs:244-600) with its exact topology and child order:
-//              DevNode 128 B (6 x float4 of child boxes, 4 child ids, axes); leaves as 144-B
-//              SoA blocks of <= 4 triangles (9 x float4: v0 v1 v2 x/y/z per lane) + the f64
+//              DevNode 128 B (per child: box, child id, axes — 32 B); leaves as 192-B blocks of
+//              <= 4 triangle records (48 B: v0 v1 v2, triangle index) + the f64
 //              interpolated-normal table. Every f32 here is exact: tobj parses positions as f32
 //              (triangle.rs:438) and box corners are min/max of those, so the f64 arithmetic of
 //              the reference is reproduced bit for bit by converting on load.
@@ -47,19 +47,21 @@ struct DevTexture {
   const uint8_t* pixels;    // IMAGE: RGB8 rows, top first (device copy)
 };
 
+// Child k of a node is two float4s, read by lane k of a quad in the cooperative traversal (one
+// 64-B load per quad per float4 row): lo[k] = (min x, min y, min z, max x), hi[k] = (max y,
+// max z, child id bits, axes bits). Empty children have +inf boxes (QBVHNode::new, qbvh.rs:570).
 struct alignas(16) DevNode {
-  float bmin[3][4];   // [axis][child]
-  float bmax[3][4];
-  uint32_t child[4];  // inner: node index; leaf: 1<<31 | count<<27 | leaf index
-  uint32_t axes;      // top | left << 2 | right << 4
-  uint32_t pad[3];
+  float lo[4][4];
+  float hi[4][4];  // [k][2]: inner: node index; leaf: 1<<31 | count<<27 | leaf index; [k][3]: axes
 };
 static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
+// A leaf is 4 triangle records of 12 floats (48 B, three float4s): v0 v1 v2 (x y z each), the
+// sorted triangle index (bits), 2 pad. Lane k of a quad reads record k.
+constexpr int kLeafFloats = 48;
 
 struct DevMesh {
   const DevNode* nodes;
-  const float* leaves;        // 36 floats per leaf: [v0x v0y v0z v1x v1y v1z v2x v2y v2z][4 lanes]
-  const uint32_t* leaf_first; // first (sorted) triangle index of each leaf
+  const float* leaves;        // kLeafFloats per leaf (see DevNode)
   const double* normals;      // 9 per sorted triangle: n0 n1 n2
   uint32_t root;              // the last node pushed (qbvh.rs:384)
   uint32_t n_nodes;

@@ -567,18 +567,64 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
   else { h.n = neg(outward); h.ff = false; }
 }
 
-// --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543), per lane
+// --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543)
 struct Stats { unsigned long long v[8]; };
 enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };
 
+// ORDER_TABLE (qbvh.rs:14-16) row for a node's split axes and the ray's octant: four nibbles, the
+// child pushed k-th in nibble k (push_hit_children, qbvh.rs:18-31).
+__device__ __forceinline__ uint32_t ray_octant(const double rd[3]) {
+  return (rd[0] >= 0.0 ? 1u : 0u) | (rd[1] >= 0.0 ? 2u : 0u) | (rd[2] >= 0.0 ? 4u : 0u);
+}
+__device__ __forceinline__ uint32_t push_order(uint32_t axes, uint32_t pos) {
+  const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
+  const uint32_t top = axes & 3u, left = (axes >> 2) & 3u, right = (axes >> 4) & 3u;
+  const uint32_t idx = 4u * ((pos >> top) & 1u) + 2u * ((pos >> left) & 1u) + ((pos >> right) & 1u);
+  return (uint32_t)(((idx < 4 ? ORDER_LO : ORDER_HI) >> (16u * (idx & 3u))) & 0xFFFFu);
+}
+// One child's slab test in f64 on its f32 box (AABB::hit as qbvh.rs:430-470 evaluates it per lane).
+__device__ __forceinline__ bool child_hit(float4 lo, float4 hi, const double ro[3], const double inv[3], double tmin,
+                                          double tmax) {
+  const float bmn[3] = {lo.x, lo.y, lo.z}, bmx[3] = {lo.w, hi.x, hi.y};
+  double l = tmin, h = tmax;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double t0 = ((double)bmn[j] - ro[j]) * inv[j], t1 = ((double)bmx[j] - ro[j]) * inv[j];
+    l = fmax(l, fmin(t0, t1));
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double t0 = ((double)bmn[j] - ro[j]) * inv[j], t1 = ((double)bmx[j] - ro[j]) * inv[j];
+    h = fmin(h, fmax(t0, t1));
+  }
+  return h > l;
+}
+// Möller–Trumbore on one leaf record (hitx4's lane, qbvh.rs:475-540): a hit needs t in
+// [t_min, t_max) — strict at t_max, so an equal t later in the leaf or tree does not replace.
+__device__ __forceinline__ bool leaf_tri_hit(float4 p0, float4 p1, float4 p2, const double ro[3], const double rd[3],
+                                             double tmin, double tmax, double& t, double& u, double& v) {
+  const double v0x = p0.x, v0y = p0.y, v0z = p0.z;
+  const double e1x = (double)p0.w - v0x, e1y = (double)p1.x - v0y, e1z = (double)p1.y - v0z;
+  const double e2x = (double)p1.z - v0x, e2y = (double)p1.w - v0y, e2z = (double)p2.x - v0z;
+  const double hx = rd[1] * e2z - rd[2] * e2y, hy = rd[2] * e2x - rd[0] * e2z, hz = rd[0] * e2y - rd[1] * e2x;
+  const double a = e1x * hx + e1y * hy + e1z * hz;
+  const double f = 1.0 / a;
+  const double sx = ro[0] - v0x, sy = ro[1] - v0y, sz = ro[2] - v0z;
+  u = f * (sx * hx + sy * hy + sz * hz);
+  const double qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
+  v = f * (rd[0] * qx + rd[1] * qy + rd[2] * qz);
+  t = f * (e2x * qx + e2y * qy + e2z * qz);
+  return !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 && t >= tmin && tmax > t;
+}
+
+// Per-lane walk (ConstantMedium boundaries, which hit their mesh from divergent code): one lane,
+// one ray, a 32-slot stack in LDS laid out [slot][lane].
 template <bool STATS>
 __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin, double tmax, double& t_hit,
                                     uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st) {
-  // ORDER_TABLE (qbvh.rs:14-16), two 16-bit entries per nibble group packed in 64-bit words.
-  const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
   const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
   const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};
-  const uint32_t pos = (rd[0] >= 0.0 ? 1u : 0u) | (rd[1] >= 0.0 ? 2u : 0u) | (rd[2] >= 0.0 ? 4u : 0u);
+  const uint32_t pos = ray_octant(rd);
   bool found = false;
   int cursor = 0;
   stk[0] = M.root;
@@ -586,69 +632,32 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
     const uint32_t id = stk[cursor * 64];
     if (id >> 31) {
       const uint32_t count = (id >> 27) & 0xFu, li = id & ((1u << 27) - 1u);
-      const float4* L = reinterpret_cast<const float4*>(M.leaves + 36 * (size_t)li);
-      const float4 q0 = L[0], q1 = L[1], q2 = L[2], q3 = L[3], q4 = L[4], q5 = L[5], q6 = L[6], q7 = L[7], q8 = L[8];
-      const float lanes[9][4] = {{q0.x, q0.y, q0.z, q0.w}, {q1.x, q1.y, q1.z, q1.w}, {q2.x, q2.y, q2.z, q2.w},
-                                 {q3.x, q3.y, q3.z, q3.w}, {q4.x, q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z, q5.w},
-                                 {q6.x, q6.y, q6.z, q6.w}, {q7.x, q7.y, q7.z, q7.w}, {q8.x, q8.y, q8.z, q8.w}};
+      const float4* L = reinterpret_cast<const float4*>(M.leaves + kLeafFloats * (size_t)li);
       if (STATS) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) {
-        if (i >= count) break;
-        const double v0x = lanes[0][i], v0y = lanes[1][i], v0z = lanes[2][i];
-        const double e1x = (double)lanes[3][i] - v0x, e1y = (double)lanes[4][i] - v0y, e1z = (double)lanes[5][i] - v0z;
-        const double e2x = (double)lanes[6][i] - v0x, e2y = (double)lanes[7][i] - v0y, e2z = (double)lanes[8][i] - v0z;
-        const double hx = rd[1] * e2z - rd[2] * e2y, hy = rd[2] * e2x - rd[0] * e2z, hz = rd[0] * e2y - rd[1] * e2x;
-        const double a = e1x * hx + e1y * hy + e1z * hz;
-        const double f = 1.0 / a;
-        const double sx = ro[0] - v0x, sy = ro[1] - v0y, sz = ro[2] - v0z;
-        const double u = f * (sx * hx + sy * hy + sz * hz);
-        const double qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
-        const double v = f * (rd[0] * qx + rd[1] * qy + rd[2] * qz);
-        const double t = f * (e2x * qx + e2y * qy + e2z * qz);
-        // hitx4 (a, u, v, t range against the t_max at leaf entry) && t_max > t (strict): the
-        // current t_max never exceeds the entry value, so the strict test subsumes `t <= t_max`.
-        const bool hit = !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 &&
-                         t >= tmin && tmax > t;
-        if (hit) {
+      for (uint32_t i = 0; i < count; ++i) {  // the running t_max: the first of equal hits stays
+        double t, u, v;
+        const float4 p2 = L[3 * i + 2];
+        if (leaf_tri_hit(L[3 * i], L[3 * i + 1], p2, ro, rd, tmin, tmax, t, u, v)) {
           tmax = t;
           t_hit = t; u_hit = u; v_hit = v;
-          tri = M.leaf_first[li] + i;
+          tri = __float_as_uint(p2.y);
           found = true;
         }
       }
     } else {
       const float4* N = reinterpret_cast<const float4*>(M.nodes + id);
-      const float4 mnx = N[0], mny = N[1], mnz = N[2], mxx = N[3], mxy = N[4], mxz = N[5];
-      const uint4 ch = reinterpret_cast<const uint4*>(N)[6];
-      const uint32_t axes = reinterpret_cast<const uint32_t*>(N)[28];
       if (STATS) st.v[ST_NODES]++;
-      const float bmn[3][4] = {{mnx.x, mnx.y, mnx.z, mnx.w}, {mny.x, mny.y, mny.z, mny.w}, {mnz.x, mnz.y, mnz.z, mnz.w}};
-      const float bmx[3][4] = {{mxx.x, mxx.y, mxx.z, mxx.w}, {mxy.x, mxy.y, mxy.z, mxy.w}, {mxz.x, mxz.y, mxz.z, mxz.w}};
       bool hk[4];
+      uint32_t chs[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        double lo = tmin, hi = tmax;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double t0 = ((double)bmn[j][k] - ro[j]) * inv[j];
-          const double t1 = ((double)bmx[j][k] - ro[j]) * inv[j];
-          lo = fmax(lo, fmin(t0, t1));
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double t0 = ((double)bmn[j][k] - ro[j]) * inv[j];
-          const double t1 = ((double)bmx[j][k] - ro[j]) * inv[j];
-          hi = fmin(hi, fmax(t0, t1));
-        }
-        hk[k] = hi > lo;
+        const float4 hi = N[4 + k];
+        hk[k] = child_hit(N[k], hi, ro, inv, tmin, tmax);
+        chs[k] = __float_as_uint(hi.z);
       }
-      const uint32_t top = axes & 3u, left = (axes >> 2) & 3u, right = (axes >> 4) & 3u;
-      const uint32_t idx = 4u * ((pos >> top) & 1u) + 2u * ((pos >> left) & 1u) + ((pos >> right) & 1u);
-      const uint32_t enc = (uint32_t)(((idx < 4 ? ORDER_LO : ORDER_HI) >> (16u * (idx & 3u))) & 0xFFFFu);
-      const uint32_t chs[4] = {ch.x, ch.y, ch.z, ch.w};
+      const uint32_t enc = push_order(__float_as_uint(N[4].w), pos);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {  // push_hit_children (qbvh.rs:18-31)
+      for (int k = 0; k < 4; ++k) {
         const uint32_t i = (enc >> (4 * k)) & 0xFu;
         const bool hi = (i == 0) ? hk[0] : (i == 1) ? hk[1] : (i == 2) ? hk[2] : hk[3];
         const uint32_t c = (i == 0) ? chs[0] : (i == 1) ? chs[1] : (i == 2) ? chs[2] : chs[3];
@@ -659,6 +668,143 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
     cursor -= 1;
   }
   return found;
+}
+
+// Cooperative walk: a quad of lanes (4 consecutive) walks ONE ray, lane k of the quad taking
+// child k of an inner node (the QBVH's 4-wide box test, qbvh.rs:430-470, as 4 lanes) or
+// triangle k of a leaf (hitx4, qbvh.rs:475-540). The wave's rays are staged in LDS and handed
+// to quads as they finish (16 quads, a ballot per round), so the wave's cost is its rays' total
+// step count / 16 rather than 64 x its slowest ray. Per ray the node order, the t_max used at
+// each test and the tie rule are the per-lane walk's: the leaf's winner is the smallest t among
+// its hits with the lowest index on ties — what the sequential strict `t_max > t` loop keeps.
+// Call from converged code (all 64 lanes); `want` selects the lanes that have a ray.
+struct CoopRay { double o[3], d[3], inv[3], tmax; };  // result: o = (t, u, v), d[0] = found << 32 | tri
+constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
+constexpr int kCoopBytes = kCoopRayBytes + kStackSlots * 16 * 4;  // + per-quad stacks [slot][quad]
+static_assert(kCoopBytes <= kStackSlots * 64 * 4, "cooperative walk must fit the wave's stack region");
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double quad_perm(double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  const uint64_t lo = quad_perm<CTRL>((uint32_t)b), hi = quad_perm<CTRL>((uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(lo | (hi << 32)));
+}
+// (t, key) lexicographic minimum with the partner lane CTRL names, carrying u, v, tri.
+template <int CTRL>
+__device__ __forceinline__ void quad_min(double& t, uint32_t& key, double& u, double& v, uint32_t& tri) {
+  const double ot = quad_perm<CTRL>(t), ou = quad_perm<CTRL>(u), ov = quad_perm<CTRL>(v);
+  const uint32_t ok = quad_perm<CTRL>(key), otri = quad_perm<CTRL>(tri);
+  if (ot < t || (ot == t && ok < key)) { t = ot; key = ok; u = ou; v = ov; tri = otri; }
+}
+
+template <bool STATS>
+__device__ __noinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
+                                       bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
+                                       uint8_t* __restrict__ lds, Stats& st) {
+  found = false;
+  const uint64_t act = __ballot(want);
+  if (act == 0) return;
+  const uint32_t lane = __lane_id();
+  CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
+  uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
+  const uint32_t n = (uint32_t)__popcll(act);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  if (want) {
+    CoopRay& s = rays[rank];
+    s.o[0] = r.o.x; s.o[1] = r.o.y; s.o[2] = r.o.z;
+    s.d[0] = r.d.x; s.d[1] = r.d.y; s.d[2] = r.d.z;
+    s.inv[0] = 1.0 / r.d.x; s.inv[1] = 1.0 / r.d.y; s.inv[2] = 1.0 / r.d.z;
+    s.tmax = tmax_in;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t q = lane >> 2, c = lane & 3u;
+  uint32_t ray = q, next = 16;
+  double ro[3], rd[3], inv[3], tmax = 0.0, bt = 0.0, bu = 0.0, bv = 0.0;
+  uint32_t pos = 0, node = 0, btri = 0;
+  int cursor = 0;
+  bool fnd = false;
+  auto take = [&]() {
+    const CoopRay& s = rays[ray];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { ro[j] = s.o[j]; rd[j] = s.d[j]; inv[j] = s.inv[j]; }
+    tmax = s.tmax;
+    pos = ray_octant(rd);
+    node = M.root;
+    cursor = 0;
+    fnd = false;
+  };
+  if (ray < n) take();
+  for (;;) {
+    const bool has = ray < n;
+    if (__ballot(has) == 0) break;
+    bool fin = false;
+    if (has) {  // quad-uniform from here on
+      if (node >> 31) {
+        const uint32_t count = (node >> 27) & 0xFu, li = node & ((1u << 27) - 1u);
+        double t = INFINITY, u = 0.0, v = 0.0;
+        uint32_t key = 4u, id = 0u;
+        if (c < count) {
+          const float4* R = reinterpret_cast<const float4*>(M.leaves + kLeafFloats * (size_t)li) + 3 * c;
+          const float4 p0 = R[0], p1 = R[1], p2 = R[2];
+          double tt, uu, vv;
+          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tmax, tt, uu, vv)) {
+            t = tt; u = uu; v = vv; key = c; id = __float_as_uint(p2.y);
+          }
+        }
+        if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
+        quad_min<0xB1>(t, key, u, v, id);  // quad_perm [1,0,3,2]
+        quad_min<0x4E>(t, key, u, v, id);  // quad_perm [2,3,0,1]
+        if (key < 4u) { tmax = t; bt = t; bu = u; bv = v; btri = id; fnd = true; }
+      } else {
+        const float4* N = reinterpret_cast<const float4*>(M.nodes + node);
+        const float4 lo = N[c], hi = N[4 + c];
+        const bool hk = child_hit(lo, hi, ro, inv, tmin, tmax);
+        const uint32_t hits = (uint32_t)(__ballot(hk) >> (4u * q)) & 0xFu;
+        const uint32_t enc = push_order(__float_as_uint(hi.w), pos);
+        uint32_t kc = 0, ordered = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t i = (enc >> (4 * k)) & 0xFu;
+          kc = i == c ? k : kc;
+          ordered |= ((hits >> i) & 1u) << k;
+        }
+        if (hk) qstk[(cursor + (int)__popc(ordered & ((1u << kc) - 1u))) * 16 + (int)q] = __float_as_uint(hi.z);
+        cursor += (int)__popc(hits);
+        if (STATS && c == 0) st.v[ST_NODES]++;
+      }
+      if (cursor == 0) {
+        fin = true;
+      } else {
+        cursor -= 1;
+        node = qstk[cursor * 16 + (int)q];
+      }
+    }
+    if (fin && c == 0) {
+      CoopRay& s = rays[ray];
+      s.o[0] = bt; s.o[1] = bu; s.o[2] = bv;
+      s.d[0] = __longlong_as_double((long long)(fnd ? ((1ull << 32) | btri) : 0ull));
+    }
+    const uint64_t fm = __ballot(fin && c == 0);
+    if (fm) {
+      if (fin) {
+        ray = next + (uint32_t)__popcll(fm & ((1ull << (4u * q)) - 1ull));
+        if (ray < n) take();
+      }
+      next += (uint32_t)__popcll(fm);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (want) {
+    const CoopRay& s = rays[rank];
+    const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
+    found = (res >> 32) != 0;
+    t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
+    tri = (uint32_t)res;
+  }
 }
 
 // The QBVH leaf record (qbvh.rs:500-540): barycentric normal of the winning triangle, facing
@@ -751,25 +897,40 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // EXT: the scene has media / noise textures / isotropic materials (DevScene::has_ext); kernels
 // for the other scenes are built without those paths (they cost the cornell box 12 % as
 // dead-but-compiled code: registers and spills).
+// HAS_MESH: called from converged code by all 64 lanes, `want` marking the lanes with a query —
+// meshes are walked cooperatively (qbvh_coop) by the whole wave, the other objects per lane.
 template <bool HAS_MESH, bool STATS, bool EXT>
-__device__ __forceinline__ bool world_closest(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
-                                              uint32_t* stk, Stats& st, const QueryCtx& q) {
+__device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
+                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
   for (uint32_t i = 0; i < S.n_objects; ++i) {
     const DevObject& o = S.objects[i];
     const uint32_t kind = o.kind, nxf = o.n_xf;
-    const Ray lr = to_local(o, nxf, r);
-    double t, u = 0.0, v = 0.0;
-    uint32_t sub = 0;
-    const bool hit = (EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM)
-                         ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                         : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
-    if (hit) {
-      closest = t;
-      id.obj = i; id.sub = sub; id.u = u; id.v = v;
-      found = true;
+    const bool medium = EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM;
+    if (HAS_MESH && kind == YART_PRIM_MESH && !medium) {  // wave-uniform
+      const Ray lr = to_local(o, nxf, r);
+      bool hit;
+      double t, u, v;
+      uint32_t sub;
+      qbvh_coop<STATS>(S.meshes[o.mesh], want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
+      if (hit) {
+        closest = t;
+        id.obj = i; id.sub = sub; id.u = u; id.v = v;
+        found = true;
+      }
+    } else if (want) {
+      const Ray lr = to_local(o, nxf, r);
+      double t, u = 0.0, v = 0.0;
+      uint32_t sub = 0;
+      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+      if (hit) {
+        closest = t;
+        id.obj = i; id.sub = sub; id.u = u; id.v = v;
+        found = true;
+      }
     }
   }
   id.t = closest;
@@ -841,7 +1002,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
-  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS, false>(S, r, tmin, tmax, id, stk, st, QueryCtx{});
+  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
   float inv[3];
   bool use[3];
 #pragma unroll
@@ -919,13 +1080,13 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
 }
 
 template <bool HAS_MESH, bool BVH, bool STATS, bool EXT>
-__device__ __forceinline__ bool world_hit(const DevScene& S, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, Stats& st, const QueryCtx& q) {
+__device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
+                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
   HitId id;
-  if constexpr (BVH) {  // no media in BVH scenes (capi.cpp)
+  if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT>(S, r, tmin, tmax, id, stk, st, q)) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT>(S, want, r, tmin, tmax, id, stk, coop, st, q) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -1183,6 +1344,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
   uint32_t* stk = &s_stack[(HAS_MESH || BVH) ? (wave * kStackSlots * 64 + lane) : 0];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kStackSlots * 64 : 0]);
   Stats st;
   if (STATS) for (int i = 0; i < 8; ++i) st.v[i] = 0;
 
@@ -1208,7 +1370,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   double hu = 0.0, hv = 0.0;            // its texture coordinates (EXT)
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
 
-  while (alive) {
+  // The loop exits wave-uniformly: a lane without work stays in it with `run` false, so the
+  // mesh walk (qbvh_coop) is reached by all 64 lanes together.
+  for (;;) {
     if (DYN) {
       uint64_t m = drained ? 0ull : __ballot(need);
       while (m) {  // wave-uniform: hand out jobs until every asking lane has one
@@ -1244,133 +1408,139 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         next_job += given < avail ? given : avail;
         m = __ballot(need);
       }
-      if (need) break;  // the queue is drained: no job for this lane
     }
-    // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
-    // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
-    // found (phase max_depth - depth + 1, its bounce level).
-    rng_phase(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
+    const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
+    if (__ballot(run) == 0) break;
     double R = 0.0;
-    bool term = false;
-    if (fresh) {  // main.rs:692-698
-      const double tx = (double)x + gen_f64(g);
-      const double u = tx / (double)(W - 1);
-      const double ty = (double)y + gen_f64(g);
-      const double v = 1.0 - ty / (double)(H - 1);
-      const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
-      ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
-      T = 1.0;
-      depth = A.max_depth;
-      fresh = false;
-    } else {  // scatter at the stored hit (material.rs), main.rs:548-584
-      const DevMaterial& m = S.materials[hmat];
-      const uint32_t kind = m.kind;
-      if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-        const Onb uvw = onb_from_w(hn);
-        V3 dir;
-        double pdf_val;
-        if (S.n_lights == 0) {
-          (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
-          dir = local(uvw, random_cosine_direction(g));
-          pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
-        } else {
-          if (gen_range(g, 0.0, 1.0) < 0.5) {
-            // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
-            const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
-            dir = light_random(S.lights[k], hp, g);
-          } else {
+    bool term = false, want = false;
+    if (run) {
+      // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
+      // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
+      // found (phase max_depth - depth + 1, its bounce level).
+      rng_phase(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
+      if (fresh) {  // main.rs:692-698
+        const double tx = (double)x + gen_f64(g);
+        const double u = tx / (double)(W - 1);
+        const double ty = (double)y + gen_f64(g);
+        const double v = 1.0 - ty / (double)(H - 1);
+        const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
+        ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
+        T = 1.0;
+        depth = A.max_depth;
+        fresh = false;
+      } else {  // scatter at the stored hit (material.rs), main.rs:548-584
+        const DevMaterial& m = S.materials[hmat];
+        const uint32_t kind = m.kind;
+        if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+          const Onb uvw = onb_from_w(hn);
+          V3 dir;
+          double pdf_val;
+          if (S.n_lights == 0) {
+            (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
             dir = local(uvw, random_cosine_direction(g));
+            pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
+          } else {
+            if (gen_range(g, 0.0, 1.0) < 0.5) {
+              // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+              const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+              dir = light_random(S.lights[k], hp, g);
+            } else {
+              dir = local(uvw, random_cosine_direction(g));
+            }
+            const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+            double sum = -0.0;
+            for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st);
+            pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
           }
-          const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-          double sum = -0.0;
-          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st);
-          pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
-        }
-        if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-          R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-          term = true;
-        } else {
-          const double cosine = dot(hn, unit(dir));  // Lambertian::scatter_pdf
-          const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-          T = ((T * att) * spdf) / pdf_val;
+          if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+            R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+            term = true;
+          } else {
+            const double cosine = dot(hn, unit(dir));  // Lambertian::scatter_pdf
+            const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+            T = ((T * att) * spdf) / pdf_val;
+            ray.o = hp;
+            ray.d = dir;
+            depth--;
+          }
+        } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
+          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+          V3 p;
+          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+            p = mk(px, py, pz);
+            if (!(len2(p) >= 1.0)) break;
+          }
+          T = T * att;
           ray.o = hp;
-          ray.d = dir;
+          ray.d = p;
+          depth--;
+        } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+          const V3 reflected = reflect(unit(ray.d), hn);
+          V3 p;
+          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+            p = mk(px, py, pz);
+            if (!(len2(p) >= 1.0)) break;
+          }
+          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+          T = T * att;
+          ray.o = hp;
+          ray.d = add(reflected, smul(m.fuzz, p));
+          depth--;
+        } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+          const double wl2 = ray.wl * ray.wl;
+          const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+          const double n = sqrt(n2);
+          V3 outward;
+          double ni_over_nt, cosine;
+          if (dot(ray.d, hn) > 0.0) {
+            outward = neg(hn); ni_over_nt = n; cosine = n * dot(ray.d, hn) / len(ray.d);
+          } else {
+            outward = hn; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, hn) / len(ray.d);
+          }
+          const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
+          const double dt = dot(uv, outward);
+          const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+          V3 out;
+          if (disc > 0.0) {
+            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
+            double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+            r0 = r0 * r0;
+            const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+            out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
+          } else {
+            out = reflect(ray.d, hn);
+          }
+          T = T * 1.0;
+          ray.o = hp;
+          ray.d = out;
           depth--;
         }
-      } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-        V3 p;
-        for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-          const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-          p = mk(px, py, pz);
-          if (!(len2(p) >= 1.0)) break;
-        }
-        T = T * att;
-        ray.o = hp;
-        ray.d = p;
-        depth--;
-      } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
-        const V3 reflected = reflect(unit(ray.d), hn);
-        V3 p;
-        for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-          const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-          p = mk(px, py, pz);
-          if (!(len2(p) >= 1.0)) break;
-        }
-        const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-        T = T * att;
-        ray.o = hp;
-        ray.d = add(reflected, smul(m.fuzz, p));
-        depth--;
-      } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
-        const double wl2 = ray.wl * ray.wl;
-        const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-        const double n = sqrt(n2);
-        V3 outward;
-        double ni_over_nt, cosine;
-        if (dot(ray.d, hn) > 0.0) {
-          outward = neg(hn); ni_over_nt = n; cosine = n * dot(ray.d, hn) / len(ray.d);
+      }
+      if (!term) {
+        if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
+          R = T * 1.0;
+          term = true;
         } else {
-          outward = hn; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, hn) / len(ray.d);
+          want = true;
         }
-        const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
-        const double dt = dot(uv, outward);
-        const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
-        V3 out;
-        if (disc > 0.0) {
-          const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
-          double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
-          r0 = r0 * r0;
-          const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
-          out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
-        } else {
-          out = reflect(ray.d, hn);
-        }
-        T = T * 1.0;
-        ray.o = hp;
-        ray.d = out;
-        depth--;
       }
     }
-    if (!term) {
-      if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
-        R = T * 1.0;
-        term = true;
-      } else {
-        Hit h;
-        int32_t which;
+    {
+      Hit h;
+      int32_t which;
+      bool hit = false;
+      const QueryCtx q{g.k0, g.k1, smp, pixel, A.max_depth - depth + 1u};
+      if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+      } else if (want) {
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+      }
+      if (want) {
         if (STATS) st.v[ST_SEGMENTS]++;
-#ifdef YART_ATTR_WORLD2
-        {
-          Hit h2; int32_t w2;
-          const uint32_t z = opaque_zero();
-          Ray r2 = ray; r2.o.x = r2.o.x + (double)z;
-          if (world_hit<HAS_MESH, BVH, STATS, EXT>(S, r2, 0.001, INFINITY, h2, w2, stk, st, QueryCtx{}) && z) A.out[w2] = h2.t;
-        }
-#endif
-        const QueryCtx q{g.k0, g.k1, smp, pixel, A.max_depth - depth + 1u};
-        if (!world_hit<HAS_MESH, BVH, STATS, EXT>(S, ray, 0.001, INFINITY, h, which, stk, st, q)) {
+        if (!hit) {
           const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
           R = T * S.background[bin];
           term = true;
@@ -1390,7 +1560,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         }
       }
     }
-    if (term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
+    if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
       double cx, cy, cz;
       cie_xyz(ray.wl, cx, cy, cz);
       double sx = cx * R, sy = cy * R, sz = cz * R;
@@ -1450,17 +1620,23 @@ __global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevSc
   __shared__ uint32_t s_stack[4 * kStackSlots * 64];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  if (i >= n) return;
-  const double* q = rays + 8 * (size_t)i;
+  const bool active = i < n;  // no early exit: the mesh walk needs the whole wave
+  const double* q = rays + 8 * (size_t)(active ? i : 0);
   Ray r{mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), 0.0, 0.0};
   Hit h;
   int32_t which = -1;
   Stats st;
-  double* o = hits + 8 * (size_t)i;
   uint32_t* stk = &s_stack[wave * kStackSlots * 64 + lane];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kStackSlots * 64]);
   const QueryCtx qc{0u, 0u, 0u, i, 0u};  // a medium's draw for query i: seed 0, sample 0, pixel i
-  const bool hit = S.world_nodes ? world_hit<false, true, false, false>(S, r, q[6], q[7], h, which, stk, st, qc)
-                                 : world_hit<true, false, false, true>(S, r, q[6], q[7], h, which, stk, st, qc);
+  bool hit = false;
+  if (S.world_nodes) {
+    if (active) hit = world_hit<false, true, false, false>(S, true, r, q[6], q[7], h, which, stk, coop, st, qc);
+  } else {
+    hit = world_hit<true, false, false, true>(S, active, r, q[6], q[7], h, which, stk, coop, st, qc);
+  }
+  if (!active) return;
+  double* o = hits + 8 * (size_t)i;
   if (hit) {
     o[0] = h.t; o[1] = h.p.x; o[2] = h.p.y; o[3] = h.p.z;
     o[4] = h.n.x; o[5] = h.n.y; o[6] = h.n.z; o[7] = h.ff ? 1.0 : 0.0;
