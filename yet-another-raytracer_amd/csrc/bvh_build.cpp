@@ -13,6 +13,16 @@ struct Box {
   double mn[3], mx[3];
 };
 
+// ORDER_TABLE (qbvh.rs:14-16) row for a node's split axes (top | left << 2 | right << 4) and a
+// ray octant (x >= 0 | y >= 0 << 1 | z >= 0 << 2): four nibbles, the child pushed k-th in nibble k
+// (push_hit_children, qbvh.rs:18-31).
+uint32_t push_order(uint32_t axes, uint32_t pos) {
+  const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
+  const uint32_t top = axes & 3u, left = (axes >> 2) & 3u, right = (axes >> 4) & 3u;
+  const uint32_t idx = 4u * ((pos >> top) & 1u) + 2u * ((pos >> left) & 1u) + ((pos >> right) & 1u);
+  return (uint32_t)(((idx < 4 ? ORDER_LO : ORDER_HI) >> (16u * (idx & 3u))) & 0xFFFFu);
+}
+
 struct Builder {
   const float* pos;
   std::vector<uint32_t> perm;      // working triangle order (sorted in place by split)
@@ -92,7 +102,13 @@ struct Builder {
       node.lo[k][0] = mn[0]; node.lo[k][1] = mn[1]; node.lo[k][2] = mn[2]; node.lo[k][3] = mx[0];
       node.hi[k][0] = mx[1]; node.hi[k][1] = mx[2];
       std::memcpy(&node.hi[k][2], &ch[k]->id, 4);
-      std::memcpy(&node.hi[k][3], &axes, 4);
+      uint32_t code = 0;  // this child's push rank for each of the 8 ray octants, 2 bits each
+      for (uint32_t pos = 0; pos < 8; ++pos) {
+        const uint32_t enc = push_order(axes, pos);
+        for (uint32_t r = 0; r < 4; ++r)
+          if (((enc >> (4 * r)) & 0xFu) == (uint32_t)k) code |= r << (2 * pos);
+      }
+      std::memcpy(&node.hi[k][3], &code, 4);
     }
     out->nodes.push_back(node);
     Box lb = ll.has && lr.has ? merge(ll.box, lr.box) : (ll.has ? ll.box : lr.box);

@@ -8,7 +8,7 @@
 //              reference recomputes the whole spectrum per lookup and reads one bin; the bins are
 //              bitwise the values it would read.
 //  Mesh BLAS   the reference's L4QBVH (qbvh.rs:244-600) with its exact topology and child order:
-//              DevNode 128 B (per child: box, child id, axes — 32 B); leaves as 192-B blocks of
+//              DevNode 128 B (per child: box, child id, push ranks — 32 B); leaves as 192-B blocks of
 //              <= 4 triangle records (48 B: v0 v1 v2, triangle index) + the f64
 //              interpolated-normal table. Every f32 here is exact: tobj parses positions as f32
 //              (triangle.rs:438) and box corners are min/max of those, so the f64 arithmetic of
@@ -49,10 +49,13 @@ struct DevTexture {
 
 // Child k of a node is two float4s, read by lane k of a quad in the cooperative traversal (one
 // 64-B load per quad per float4 row): lo[k] = (min x, min y, min z, max x), hi[k] = (max y,
-// max z, child id bits, axes bits). Empty children have +inf boxes (QBVHNode::new, qbvh.rs:570).
+// max z, child id bits, push ranks). The push rank of child k for ray octant o (bits 2o..2o+1) is
+// its position in the ORDER_TABLE row of the node's split axes (qbvh.rs:14-31), precomputed so a
+// lane needs one shift instead of the table walk. Empty children have +inf boxes (QBVHNode::new,
+// qbvh.rs:570-572).
 struct alignas(16) DevNode {
   float lo[4][4];
-  float hi[4][4];  // [k][2]: inner: node index; leaf: 1<<31 | count<<27 | leaf index; [k][3]: axes
+  float hi[4][4];  // [k][2]: inner: node index; leaf: 1<<31 | count<<27 | leaf index; [k][3]: ranks
 };
 static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
 // A leaf is 4 triangle records of 12 floats (48 B, three float4s): v0 v1 v2 (x y z each), the

@@ -571,16 +571,19 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
 struct Stats { unsigned long long v[8]; };
 enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };
 
-// ORDER_TABLE (qbvh.rs:14-16) row for a node's split axes and the ray's octant: four nibbles, the
-// child pushed k-th in nibble k (push_hit_children, qbvh.rs:18-31).
+// Ray octant: x >= 0 | y >= 0 << 1 | z >= 0 << 2, the ORDER_TABLE column (qbvh.rs:14-31); a
+// child's push rank for it is 2 bits of its node record (bvh_build.cpp).
 __device__ __forceinline__ uint32_t ray_octant(const double rd[3]) {
   return (rd[0] >= 0.0 ? 1u : 0u) | (rd[1] >= 0.0 ? 2u : 0u) | (rd[2] >= 0.0 ? 4u : 0u);
 }
-__device__ __forceinline__ uint32_t push_order(uint32_t axes, uint32_t pos) {
-  const uint64_t ORDER_LO = 0x1032102301320123ull, ORDER_HI = 0x3210231032012301ull;
-  const uint32_t top = axes & 3u, left = (axes >> 2) & 3u, right = (axes >> 4) & 3u;
-  const uint32_t idx = 4u * ((pos >> top) & 1u) + 2u * ((pos >> left) & 1u) + ((pos >> right) & 1u);
-  return (uint32_t)(((idx < 4 ? ORDER_LO : ORDER_HI) >> (16u * (idx & 3u))) & 0xFFFFu);
+// BLAS records are read through global (address space 1) pointers: a generic pointer makes the
+// compiler emit flat loads, which also count against the LDS counter and serialize with the
+// traversal stack.
+typedef float vfloat4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) vfloat4* gfloat4p;
+__device__ __forceinline__ float4 ld4(gfloat4p p, size_t i) {
+  const vfloat4 v = p[i];
+  return make_float4(v.x, v.y, v.z, v.w);
 }
 // One child's slab test in f64 on its f32 box (AABB::hit as qbvh.rs:430-470 evaluates it per lane).
 __device__ __forceinline__ bool child_hit(float4 lo, float4 hi, const double ro[3], const double inv[3], double tmin,
@@ -625,6 +628,7 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
   const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
   const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};
   const uint32_t pos = ray_octant(rd);
+  const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
   bool found = false;
   int cursor = 0;
   stk[0] = M.root;
@@ -632,12 +636,12 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
     const uint32_t id = stk[cursor * 64];
     if (id >> 31) {
       const uint32_t count = (id >> 27) & 0xFu, li = id & ((1u << 27) - 1u);
-      const float4* L = reinterpret_cast<const float4*>(M.leaves + kLeafFloats * (size_t)li);
+      const gfloat4p L = leaves + (kLeafFloats / 4) * (size_t)li;
       if (STATS) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
       for (uint32_t i = 0; i < count; ++i) {  // the running t_max: the first of equal hits stays
         double t, u, v;
-        const float4 p2 = L[3 * i + 2];
-        if (leaf_tri_hit(L[3 * i], L[3 * i + 1], p2, ro, rd, tmin, tmax, t, u, v)) {
+        const float4 p2 = ld4(L, 3 * i + 2);
+        if (leaf_tri_hit(ld4(L, 3 * i), ld4(L, 3 * i + 1), p2, ro, rd, tmin, tmax, t, u, v)) {
           tmax = t;
           t_hit = t; u_hit = u; v_hit = v;
           tri = __float_as_uint(p2.y);
@@ -645,24 +649,22 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
         }
       }
     } else {
-      const float4* N = reinterpret_cast<const float4*>(M.nodes + id);
+      const gfloat4p N = nodes + 8 * (size_t)id;
       if (STATS) st.v[ST_NODES]++;
       bool hk[4];
-      uint32_t chs[4];
+      uint32_t chs[4], rank[4], ordered = 0;  // ordered: bit r = the child of push rank r was hit
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float4 hi = N[4 + k];
-        hk[k] = child_hit(N[k], hi, ro, inv, tmin, tmax);
+        const float4 hi = ld4(N, 4 + k);
+        hk[k] = child_hit(ld4(N, k), hi, ro, inv, tmin, tmax);
         chs[k] = __float_as_uint(hi.z);
+        rank[k] = (__float_as_uint(hi.w) >> (2u * pos)) & 3u;
+        ordered |= (hk[k] ? 1u : 0u) << rank[k];
       }
-      const uint32_t enc = push_order(__float_as_uint(N[4].w), pos);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t i = (enc >> (4 * k)) & 0xFu;
-        const bool hi = (i == 0) ? hk[0] : (i == 1) ? hk[1] : (i == 2) ? hk[2] : hk[3];
-        const uint32_t c = (i == 0) ? chs[0] : (i == 1) ? chs[1] : (i == 2) ? chs[2] : chs[3];
-        if (hi) { stk[cursor * 64] = c; cursor++; }
-      }
+      for (int k = 0; k < 4; ++k)  // pushed in rank order: slot = hit children of lower rank
+        if (hk[k]) stk[(cursor + (int)__popc(ordered & ((1u << rank[k]) - 1u))) * 64] = chs[k];
+      cursor += (int)__popc(ordered);
     }
     if (cursor == 0) break;
     cursor -= 1;
@@ -693,16 +695,26 @@ __device__ __forceinline__ double quad_perm(double x) {
   const uint64_t lo = quad_perm<CTRL>((uint32_t)b), hi = quad_perm<CTRL>((uint32_t)(b >> 32));
   return __longlong_as_double((long long)(lo | (hi << 32)));
 }
-// (t, key) lexicographic minimum with the partner lane CTRL names, carrying u, v, tri.
+// (t, key) lexicographic minimum with the partner lane CTRL names.
 template <int CTRL>
-__device__ __forceinline__ void quad_min(double& t, uint32_t& key, double& u, double& v, uint32_t& tri) {
-  const double ot = quad_perm<CTRL>(t), ou = quad_perm<CTRL>(u), ov = quad_perm<CTRL>(v);
-  const uint32_t ok = quad_perm<CTRL>(key), otri = quad_perm<CTRL>(tri);
-  if (ot < t || (ot == t && ok < key)) { t = ot; key = ok; u = ou; v = ov; tri = otri; }
+__device__ __forceinline__ void quad_min(double& t, uint32_t& key) {
+  const double ot = quad_perm<CTRL>(t);
+  const uint32_t ok = quad_perm<CTRL>(key);
+  const bool other = (ot < t) | ((ot == t) & (ok < key));
+  t = other ? ot : t;
+  key = other ? ok : key;
 }
+#ifndef YART_COOP_LEAF_MIN
+#define YART_COOP_LEAF_MIN 1  // quads waiting at a leaf before a round runs the leaf branch
+#endif
 
+#ifdef YART_COOP_NOINLINE
+#define YART_COOP_ATTR __noinline__
+#else
+#define YART_COOP_ATTR __forceinline__  // inlined: +4% david, +11% bunny over a call (caller spills)
+#endif
 template <bool STATS>
-__device__ __noinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
+__device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
                                        uint8_t* __restrict__ lds, Stats& st) {
   found = false;
@@ -721,10 +733,14 @@ __device__ __noinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r
     s.tmax = tmax_in;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
+  // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
+  const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
+  const uint32_t root = M.root;
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
   double ro[3], rd[3], inv[3], tmax = 0.0, bt = 0.0, bu = 0.0, bv = 0.0;
-  uint32_t pos = 0, node = 0, btri = 0;
+  uint32_t pos = 0, node = 0, btri = 0, win = 0;  // win: the quad lane holding the best hit
   int cursor = 0;
   bool fnd = false;
   auto take = [&]() {
@@ -733,57 +749,84 @@ __device__ __noinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r
     for (int j = 0; j < 3; ++j) { ro[j] = s.o[j]; rd[j] = s.d[j]; inv[j] = s.inv[j]; }
     tmax = s.tmax;
     pos = ray_octant(rd);
-    node = M.root;
+    node = root;
     cursor = 0;
     fnd = false;
+    win = 0;
   };
   if (ray < n) take();
   for (;;) {
     const bool has = ray < n;
     if (__ballot(has) == 0) break;
     bool fin = false;
-    if (has) {  // quad-uniform from here on
+#if YART_COOP_LEAF_MIN > 1
+    // Leaf rounds wait until enough quads sit at a leaf (or none can descend): a round pays for
+    // each branch any quad takes, and the leaf branch is the expensive one.
+    const uint64_t at_leaf = __ballot(has && c == 0 && (node >> 31));
+    const uint64_t at_inner = __ballot(has && c == 0 && !(node >> 31));
+    const bool leaf_round = __popcll(at_leaf) >= YART_COOP_LEAF_MIN || at_inner == 0;
+#else
+    const bool leaf_round = true;
+#endif
+    if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
+      bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
         const uint32_t count = (node >> 27) & 0xFu, li = node & ((1u << 27) - 1u);
         double t = INFINITY, u = 0.0, v = 0.0;
         uint32_t key = 4u, id = 0u;
         if (c < count) {
-          const float4* R = reinterpret_cast<const float4*>(M.leaves + kLeafFloats * (size_t)li) + 3 * c;
-          const float4 p0 = R[0], p1 = R[1], p2 = R[2];
+          const gfloat4p R = leaves + (kLeafFloats / 4) * (size_t)li + 3 * c;
+          float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
+          // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
+          asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
+                       "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y));
           double tt, uu, vv;
           if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tmax, tt, uu, vv)) {
             t = tt; u = uu; v = vv; key = c; id = __float_as_uint(p2.y);
           }
         }
         if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
-        quad_min<0xB1>(t, key, u, v, id);  // quad_perm [1,0,3,2]
-        quad_min<0x4E>(t, key, u, v, id);  // quad_perm [2,3,0,1]
-        if (key < 4u) { tmax = t; bt = t; bu = u; bv = v; btri = id; fnd = true; }
-      } else {
-        const float4* N = reinterpret_cast<const float4*>(M.nodes + node);
-        const float4 lo = N[c], hi = N[4 + c];
-        const bool hk = child_hit(lo, hi, ro, inv, tmin, tmax);
-        const uint32_t hits = (uint32_t)(__ballot(hk) >> (4u * q)) & 0xFu;
-        const uint32_t enc = push_order(__float_as_uint(hi.w), pos);
-        uint32_t kc = 0, ordered = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t i = (enc >> (4 * k)) & 0xFu;
-          kc = i == c ? k : kc;
-          ordered |= ((hits >> i) & 1u) << k;
+        quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
+        quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
+        if (key < 4u) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
+          tmax = t; fnd = true; win = key;
+          if (c == key) { bt = t; bu = u; bv = v; btri = id; }
         }
-        if (hk) qstk[(cursor + (int)__popc(ordered & ((1u << kc) - 1u))) * 16 + (int)q] = __float_as_uint(hi.z);
-        cursor += (int)__popc(hits);
-        if (STATS && c == 0) st.v[ST_NODES]++;
-      }
-      if (cursor == 0) {
-        fin = true;
       } else {
-        cursor -= 1;
-        node = qstk[cursor * 16 + (int)q];
+        const gfloat4p N = nodes + 8 * (size_t)node;
+        const float4 lo = ld4(N, c);
+        float4 hi = ld4(N, 4 + c);
+        asm volatile("" : "+v"(hi.z), "+v"(hi.w));  // child id and ranks with the box, one round
+        const bool hk = child_hit(lo, hi, ro, inv, tmin, tmax);
+        const uint32_t rk = (__float_as_uint(hi.w) >> (2u * pos)) & 3u;
+        uint32_t ordered = hk ? 1u << rk : 0u;  // bit r: the child of push rank r was hit
+        ordered |= quad_perm<0xB1>(ordered);
+        ordered |= quad_perm<0x4E>(ordered);
+        if (STATS && c == 0) st.v[ST_NODES]++;
+        if (ordered) {
+          // The last child pushed is the next popped: it goes straight to `node` (its id OR-ed
+          // across the quad); the others take stack slots in rank order.
+          const uint32_t last = 31u - __clz(ordered);
+          const uint32_t child = __float_as_uint(hi.z);
+          uint32_t nx = (hk && rk == last) ? child : 0u;
+          nx |= quad_perm<0xB1>(nx);
+          nx |= quad_perm<0x4E>(nx);
+          if (hk && rk != last) qstk[(cursor + (int)__popc(ordered & ((1u << rk) - 1u))) * 16 + (int)q] = child;
+          cursor += (int)__popc(ordered) - 1;
+          node = nx;
+          popped = true;
+        }
+      }
+      if (!popped) {
+        if (cursor == 0) {
+          fin = true;
+        } else {
+          cursor -= 1;
+          node = qstk[cursor * 16 + (int)q];
+        }
       }
     }
-    if (fin && c == 0) {
+    if (fin && c == (fnd ? win : 0u)) {
       CoopRay& s = rays[ray];
       s.o[0] = bt; s.o[1] = bu; s.o[2] = bv;
       s.d[0] = __longlong_as_double((long long)(fnd ? ((1ull << 32) | btri) : 0ull));
