@@ -51,6 +51,55 @@ def test_device_sqrt_and_div_are_ieee(dev):
     np.testing.assert_array_equal(_probe(dev, 1, a, b), want)
 
 
+def _edge_values(rng, n):
+    """Magnitudes across the whole f64 range (denormals, the fast paths' guard edges at 2^-767,
+    2^-600, 2^-300, 2^300, 2^400, 2^600), signed zeros, inf and nan, plus ordinary values."""
+    e = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.0 ** -1022, 2.0 ** -767, 2.0 ** -768,
+                  2.0 ** -600, 2.0 ** -601, 2.0 ** -300, 2.0 ** -301, 2.0 ** 300, 2.0 ** 301, 2.0 ** 400,
+                  2.0 ** 401, 2.0 ** 600, 2.0 ** 601, 1.0, -1.0, 1e-250, 1e250, 1.7976931348623157e308])
+    mag = 2.0 ** rng.uniform(-1074, 1023, n) * rng.choice([-1.0, 1.0], n)
+    ordinary = rng.uniform(-2, 2, n)
+    picks = rng.choice(e, n)
+    return np.where(rng.random(n) < 0.2, picks, np.where(rng.random(n) < 0.5, mag, ordinary))
+
+
+def _bits(x):
+    return np.ascontiguousarray(x, dtype=np.float64).view(np.uint64)
+
+
+def test_device_fast_sqrt_unit_div_are_bitwise_ieee(dev):
+    """kernels.hip's guarded fast paths (sqrt_x, unit, div3_pos) against numpy's correctly
+    rounded operations, compared as bit patterns (sign of zero and NaN included)."""
+    rng = np.random.default_rng(11)
+    with np.errstate(all="ignore"):
+        a = np.abs(_edge_values(rng, 200000))
+        a[:8] = [0.0, -0.0, np.inf, np.nan, 5e-324, 2.0 ** -767, np.nextafter(2.0 ** -767, 0), -1.0]
+        got, want = _probe(dev, 8, a), np.sqrt(a)
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(got), nan)
+        np.testing.assert_array_equal(_bits(got[~nan]), _bits(want[~nan]))
+
+        v = _edge_values(rng, 3 * 100000).reshape(-1, 3)
+        v[:6] = [[0.0, 1.0, 0.0], [-0.0, 1.0, -0.0], [1.0, 1e-250, 0.0], [3.0, -4.0, -0.0], [2.0 ** -700, 1.0, 0.0],
+                 [0.0, 0.0, 0.0]]
+        l = np.sqrt(v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1] + v[:, 2] * v[:, 2])
+        want = (v / l[:, None]).ravel()
+        got = _probe(dev, 9, v.ravel())
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(got), nan)
+        np.testing.assert_array_equal(_bits(got[~nan]), _bits(want[~nan]))
+
+        t = _edge_values(rng, 3 * 100000)
+        s = np.abs(_edge_values(rng, 100000))
+        s[s == 0] = 1.0
+        s = np.repeat(s, 3)  # one denominator per triple, laid out like the numerators
+        want = t / s
+        got = _probe(dev, 10, t, s[::3].copy())
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(got), nan)
+        np.testing.assert_array_equal(_bits(got[~nan]), _bits(want[~nan]))
+
+
 def test_device_sin_cos_match_oracle(dev):
     rng = np.random.default_rng(4)
     a = np.concatenate([rng.uniform(0, 2 * math.pi, 50000), rng.uniform(-500, 500, 50000)])
@@ -218,6 +267,22 @@ def test_moving_spheres_match_oracle(dev):
     h, o = s.intersect(rays)
     h2, o2 = O.OracleScene(d).intersect(rays)
     _hits_equal(h, o, h2, o2)
+
+
+@pytest.mark.parametrize("lookfrom,lookat", [((0.0, 278.0, -800.0), (0.0, 278.0, 0.0)),     # origin.x == 0
+                                             ((278.0, 278.0, -800.0), (278.0, 278.0, 0.0)),  # the preset's
+                                             ((278.0, 0.0, -800.0), (278.0, 0.0, 555.0))])   # origin.y == 0
+def test_pinhole_camera_shortcut_is_exact(dev, lookfrom, lookat):
+    """Aperture 0 without shutter time: k_render skips random_in_unit_disk (its draws and its ±0
+    offset cannot reach the ray) unless an origin or direction component is zero, where the full
+    camera.rs:82-94 path runs (a zero origin component sends every ray there). Both branches must
+    equal the oracle, which always runs the loop."""
+    p = yart.Preset("cornell-box")
+    W, H = 41, 33
+    cam = yart.make_camera(lookfrom, lookat, 40.0, W / H, 0.0, 10.0)
+    prm = yart.render_params(W, H, 3, 50)
+    s = yart.DeviceScene(p.desc)
+    np.testing.assert_array_equal(s.render(cam, prm), O.OracleScene(p.desc).render(cam, prm))
 
 
 def test_scene_info_matches_reference_qbvh(dev):

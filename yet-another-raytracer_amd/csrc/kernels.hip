@@ -38,6 +38,68 @@ __device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ V3 muls(V3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ V3 smul(double s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+// ------------------------------------------- exact fast paths for f64 sqrt and division
+// hipcc lowers f64 `sqrt` and `/` to IEEE-correct sequences (LLVM AMDGPU):
+//   sqrt: x < 2^-767 ? scale by 2^256 : x; v_rsq_f64; 2 Goldschmidt + 2 Newton fma steps; unscale;
+//         zero/+inf class fixup                                          (18 VALU instructions)
+//   n/d:  v_div_scale_f64 (d); v_rcp_f64; 2 Newton steps; v_div_scale_f64 (n); q = n·r;
+//         rem = fma(-d, q, n); v_div_fmas_f64 (= fma(rem, r, q) unless a scale fired);
+//         v_div_fixup_f64 (specials, sign)                                (11 VALU instructions)
+// Inside the ranges guarded below no scale step fires and the fixups pass the value through, so
+// the bare cores are bitwise the full sequences; outside them the full sequence runs. Quotients
+// sharing a positive denominator share its reciprocal (unit vectors: one chain, not three).
+// n = ±0 (which v_div_scale turns into NaN for v_div_fixup to repair) is exact in the core's
+// rem-negated form when d > 0: q = ±0·r, remn = d·q − n = +0, fma(−remn, r, q) = q.
+// Off by default (build with -DYART_FAST_MATH): measured on the MI355X, the per-operation guard
+// branches cost more than the shorter cores save (cornell 4,336 vs 4,436 Msamples/s, bitwise both).
+#if !defined(YART_FAST_MATH) && !defined(YART_SLOW_MATH)
+#define YART_SLOW_MATH
+#endif
+#ifndef YART_SLOW_MATH
+__device__ __forceinline__ double sqrt_core(double x) {  // x in [2^-767, inf)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double rcp_core(double d) {  // |d| in [2^-300, 2^300]
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_core_pos(double n, double d, double r) {  // d > 0, r = rcp_core(d)
+  const double q = n * r;
+  const double remn = __builtin_fma(d, q, -n);
+  return __builtin_fma(-remn, r, q);
+}
+// A numerator over a denominator in [2^-300, 2^300]: zero, or |n| in [2^-600, 2^400] (no scale,
+// quotient normal, exponent gap < 768).
+__device__ __forceinline__ bool num_ok(double n) { return n == 0.0 || (fabs(n) >= 0x1p-600 && fabs(n) <= 0x1p400); }
+__device__ __forceinline__ double sqrt_x(double x) {
+  if (x >= 0x1p-767 && x < INFINITY) return sqrt_core(x);
+  return sqrt(x);
+}
+#else
+__device__ __forceinline__ double sqrt_x(double x) { return sqrt(x); }
+#endif
+// n_i / s for a positive s shared by three quotients
+__device__ __forceinline__ void div3_pos(double& a, double& b, double& c, double s) {
+#ifndef YART_SLOW_MATH
+  if (s >= 0x1p-300 && s <= 0x1p300 && num_ok(a) && num_ok(b) && num_ok(c)) {
+    const double r = rcp_core(s);
+    a = div_core_pos(a, s, r); b = div_core_pos(b, s, r); c = div_core_pos(c, s, r);
+    return;
+  }
+#endif
+  a = a / s; b = b / s; c = c / s;
+}
 __device__ __forceinline__ V3 divs(V3 a, double s) {  // vec3.rs:109-122 (0 -> f64::MAX)
   if (s == 0.0) return mk(kF64Max, kF64Max, kF64Max);
   return mk(a.x / s, a.y / s, a.z / s);
@@ -47,8 +109,19 @@ __device__ __forceinline__ V3 cross(V3 a, V3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 __device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
-__device__ __forceinline__ V3 unit(V3 a) { double l = len(a); return mk(a.x / l, a.y / l, a.z / l); }
+__device__ __forceinline__ double len(V3 a) { return sqrt_x(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ V3 unit(V3 a) {  // vec3.rs unit_vector: a / |a|
+  const double l2 = a.x * a.x + a.y * a.y + a.z * a.z;
+#ifndef YART_SLOW_MATH
+  // l2 in [2^-600, 2^600] puts |a| in [2^-300, 2^300] (and its sqrt in the core's range)
+  if (l2 >= 0x1p-600 && l2 <= 0x1p600 && num_ok(a.x) && num_ok(a.y) && num_ok(a.z)) {
+    const double l = sqrt_core(l2), r = rcp_core(l);
+    return mk(div_core_pos(a.x, l, r), div_core_pos(a.y, l, r), div_core_pos(a.z, l, r));
+  }
+#endif
+  const double l = sqrt(l2);
+  return mk(a.x / l, a.y / l, a.z / l);
+}
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
 struct Ray { V3 o, d; double time, wl; };
@@ -286,16 +359,34 @@ __device__ __forceinline__ void philox(const Rng& r, uint32_t blk, uint32_t& o0,
   uint32_t c0 = blk, c1 = r.c1, c2 = r.c2, c3 = r.c3, k0 = r.k0, k1 = r.k1;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
+#ifdef YART_PHILOX_MAD
+    // one v_mad_u64_u32 per product instead of v_mul_hi_u32 + v_mul_lo_u32
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+#endif
     c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
   o0 = c0; o1 = c1; o2 = c2; o3 = c3;
 }
 // Start `phase` of (pixel, sample) with blocks 0 and 1 in the buffer (4 draws).
+template <bool LAUNDER>
 __device__ __forceinline__ void rng_phase(Rng& r, uint32_t pixel, uint32_t sample, uint32_t phase) {
   r.c1 = sample; r.c2 = pixel; r.c3 = phase << 2;
+#ifndef YART_NO_LAUNDER
+  if (LAUNDER) {  // the analytic linear-list kernel: +0.5 % there, -2 % on the world-BVH kernel
+  // The key is loop-invariant. Hoisted, its 20-word round schedule sat in SGPRs all kernel long and
+  // was spilled to VGPR lanes (one v_readlane, a VALU instruction, per round key per iteration).
+  // Made opaque here, the schedule is recomputed with scalar adds at each phase start.
+  r.k0 = __builtin_amdgcn_readfirstlane(r.k0);  // uniform (the seed); says so where control diverged
+  r.k1 = __builtin_amdgcn_readfirstlane(r.k1);
+  asm volatile("" : "+s"(r.k0), "+s"(r.k1));
+  }
+#endif
   philox(r, 0u, r.b0, r.b1, r.b2, r.b3);
   philox(r, 1u, r.b4, r.b5, r.b6, r.b7);
   r.c0 = 2; r.have = 4;
@@ -380,7 +471,7 @@ __device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double t
   double c = len2(oc) - radius * radius;
   double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
-  double sq = sqrt(disc);
+  double sq = sqrt_x(disc);
   t = (0.0 - half_b - sq) / a;
   if (t < tmin || tmax < t) {
     t = (0.0 - half_b + sq) / a;
@@ -393,7 +484,9 @@ __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double
   V3 center = mk(p[0], p[1], p[2]);
   double radius = p[3];
   V3 pt = at(r, t);
-  V3 outward = divs(sub(pt, center), fabs(radius));
+  V3 outward = sub(pt, center);  // (pt - center) / |radius| (vec3.rs:109-122: / 0 -> f64::MAX)
+  if (radius != 0.0) div3_pos(outward.x, outward.y, outward.z, fabs(radius));
+  else outward = mk(kF64Max, kF64Max, kF64Max);
   if (radius < 0.0) { h.n = neg(outward); h.ff = dot(r.d, outward) > 0.0; }
   else { h.n = outward; h.ff = dot(r.d, outward) < 0.0; }
   h.t = t; h.p = pt;
@@ -421,7 +514,7 @@ __device__ __forceinline__ bool moving_sphere_t(const double* p, const Ray& r, d
   const double a = len2(r.d), half_b = dot(oc, r.d), c = len2(oc) - radius * radius;
   const double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
-  const double sq = sqrt(disc);
+  const double sq = sqrt_x(disc);
   t = (0.0 - half_b - sq) / a;
   if (t < tmin || tmax < t) {
     t = (0.0 - half_b + sq) / a;
@@ -1150,10 +1243,11 @@ __device__ __forceinline__ Onb onb_from_w(V3 n) {  // onb.rs:10-21
 __device__ __forceinline__ V3 local(const Onb& b, V3 a) { return add(add(smul(a.x, b.u), smul(a.y, b.v)), smul(a.z, b.w)); }
 __device__ __forceinline__ V3 random_cosine_direction(Rng& g) {  // pdf.rs:15-25
   const double r1 = gen_f64(g), r2 = gen_f64(g);
-  const double z = sqrt(1.0 - r2);
+  const double z = sqrt_x(1.0 - r2);
   double s, c;
   sincos_det(2.0 * kPi * r1, s, c);
-  return mk(c * sqrt(r2), s * sqrt(r2), z);
+  const double sr2 = sqrt_x(r2);
+  return mk(c * sr2, s * sr2, z);
 }
 __device__ __forceinline__ double cosine_value(const Onb& b, V3 d) {  // pdf.rs:40-47
   const double cosine = dot(unit(d), b.w);
@@ -1177,7 +1271,7 @@ __device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 di
     if (STATS) st.v[ST_LIGHT]++;
     if (!sphere_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
     const double radius = o.p[3];
-    const double cos_theta_max = sqrt(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
+    const double cos_theta_max = sqrt_x(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
     const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
     return 1.0 / solid_angle;
   }
@@ -1195,10 +1289,11 @@ __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g
     const Onb uvw = onb_from_w(direction);
     const double r1 = gen_f64(g), r2 = gen_f64(g);
     const double radius = o.p[3];
-    const double z = 1.0 + r2 * (sqrt(1.0 - radius * radius / d2) - 1.0);
+    const double z = 1.0 + r2 * (sqrt_x(1.0 - radius * radius / d2) - 1.0);
     double s, c;
     sincos_det(2.0 * kPi * r1, s, c);
-    const V3 rs = mk(c * sqrt(1.0 - z * z), s * sqrt(1.0 - z * z), z);
+    const double sz = sqrt_x(1.0 - z * z);
+    const V3 rs = mk(c * sz, s * sz, z);
     return local(uvw, rs);
   }
   return mk(1.0, 0.0, 0.0);
@@ -1318,8 +1413,39 @@ __device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, 
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, smul(2.0 * dot(v, n), n)); }  // material.rs:75-77
 
 // --------------------------------------------------------------------------- sampling
-__device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double t, double wl, Rng& g,
+// The camera constants, read through an opaque kernarg-segment pointer at each use (scalar loads whose
+// SGPRs live only in the camera block). Hoisted out of the render loop they held ~40 SGPRs for the
+// whole kernel and were spilled to VGPR lanes: 22 v_readlane (VALU) per camera ray.
+constexpr size_t kKernargCam = (sizeof(DevScene) + alignof(RenderArgs) - 1) / alignof(RenderArgs) * alignof(RenderArgs) +
+                               offsetof(RenderArgs, cam);  // k_render(DevScene S, RenderArgs A): A.cam
+typedef const __attribute__((address_space(4))) yart_camera* kcam_ptr;
+__device__ __forceinline__ kcam_ptr kernarg_camera() {
+  const __attribute__((address_space(4))) char* p =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (kcam_ptr)(p + kKernargCam);
+}
+__device__ __forceinline__ V3 ld3(const __attribute__((address_space(4))) double* p) { return mk(p[0], p[1], p[2]); }
+
+template <class Cam>
+__device__ __forceinline__ Ray camera_ray(const Cam& c, double s, double t, double wl, Rng& g,
                                           bool draw_time) {  // camera.rs:82-94
+  const V3 org = ld3(c.origin);
+  const V3 d0 = sub(add(add(ld3(c.lower_left_corner), smul(s, ld3(c.horizontal))), smul(t, ld3(c.vertical))), org);
+  Ray r;
+  r.wl = wl;
+  // Pinhole (lens_radius = 0, e.g. every aperture-0 preset) with no shutter-time draw: the disk
+  // sample only reaches the ray as offset = u·(0·px) + v·(0·py) = ±0 per component, and no later
+  // draw of phase 0 depends on how many values the rejection loop consumed. org + ±0 and d0 − ±0
+  // are org and d0 whenever those components are non-zero, so the loop (and the Philox refill
+  // its fourth and fifth draws trigger) is skipped exactly; a zero component takes the full path.
+  if (c.lens_radius == 0.0 && !draw_time && org.x != 0.0 && org.y != 0.0 && org.z != 0.0 && d0.x != 0.0 &&
+      d0.y != 0.0 && d0.z != 0.0) {
+    r.o = org;
+    r.d = d0;
+    r.time = c.time0;
+    return r;
+  }
   V3 p;
   for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_disk camera.rs:25-33
     const double x = gen_range(g, -1.0, 1.0);
@@ -1329,13 +1455,10 @@ __device__ __forceinline__ Ray camera_ray(const yart_camera& c, double s, double
   }
   const V3 rd = smul(c.lens_radius, p);
   const V3 offset = add(muls(ld3(c.u), rd.x), muls(ld3(c.v), rd.y));
-  const V3 org = ld3(c.origin);
-  Ray r;
   r.o = add(org, offset);
-  r.d = sub(sub(add(add(ld3(c.lower_left_corner), smul(s, ld3(c.horizontal))), smul(t, ld3(c.vertical))), org), offset);
+  r.d = sub(d0, offset);
   // gen_range(time0..time1) (camera.rs:91): drawn only when a MovingSphere can read it
   r.time = draw_time ? gen_range(g, c.time0, c.time1) : c.time0;
-  r.wl = wl;
   return r;
 }
 
@@ -1367,6 +1490,23 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 #ifndef YART_MESH_WAVES_PER_EU
 #define YART_MESH_WAVES_PER_EU 4  // 128 VGPRs; traversal is latency-bound: +36% on david over 2
 #endif
+// Lane-occupancy probe (debug builds with -DYART_OCC only, tools/occupancy.py): per region, the
+// number of wave executions and the lanes active in them.
+enum { OCC_ITER, OCC_FRESH, OCC_LAMB, OCC_LAMB_LIGHT, OCC_LAMB_COS, OCC_DIEL, OCC_METAL, OCC_WALK, OCC_TERM, OCC_ASSIGN };
+#ifdef YART_OCC
+__device__ unsigned long long g_occ[32];
+#define OCC(k)                                                                         \
+  do {                                                                                 \
+    const uint64_t m_ = __ballot(1);                                                   \
+    if (lane == (uint32_t)__builtin_ctzll(m_)) {                                       \
+      atomicAdd(&g_occ[2 * (k)], 1ull);                                                \
+      atomicAdd(&g_occ[2 * (k) + 1], (unsigned long long)__popcll(m_));                \
+    }                                                                                  \
+  } while (0)
+#else
+#define OCC(k) do {} while (0)
+#endif
+
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
 __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[(HAS_MESH || BVH) ? 4 * kStackSlots * 64 : 1];
@@ -1400,6 +1540,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // scratch: [local_blk][sample - s_begin][slot][xyz]; DYN lanes keep their job's block
   uint32_t lane_blk = local_blk;
   uint32_t n_jobs = 0, next_job = 0;  // the wave's current unit (DYN, wave-uniform)
+  uint64_t cov = 0;                   // DYN: the unit's block slots that are rendered (wave-uniform)
   bool drained = false;               // DYN: the queue has no units left (wave-uniform)
   bool need = true;                   // DYN: this lane wants a job
   bool alive = DYN ? true : (active && smp < s_stop);
@@ -1419,6 +1560,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     if (DYN) {
       uint64_t m = drained ? 0ull : __ballot(need);
       while (m) {  // wave-uniform: hand out jobs until every asking lane has one
+        OCC(OCC_ASSIGN);
         if (next_job >= n_jobs) {  // claim the next unit
           const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
           uint32_t v = 0;
@@ -1432,6 +1574,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           const uint32_t stop = s_lo + A.chunk < s_end ? s_lo + A.chunk : s_end;
           n_jobs = (stop > s_lo ? stop - s_lo : 0) * 64;
           next_job = 0;
+          {  // the block's pixels inside the frame and the crop grid (main.rs:636-647), once per unit
+            const uint32_t cx = bx0 + (lane & 7u), cy = by0 + (lane >> 3);
+            cov = __ballot(cx < W && cy < H && covered(cx, W) && covered(cy, H));
+          }
           continue;
         }
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1445,7 +1591,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           pixel = y * W + x;
           lane_blk = local_blk;
           // a pixel outside the crop grid is skipped: the lane asks again
-          if (x < W && y < H && covered(x, W) && covered(y, H)) { fresh = true; need = false; }
+          if ((cov >> slot) & 1ull) { fresh = true; need = false; }
         }
         const uint32_t given = (uint32_t)__popcll(m);
         next_job += given < avail ? given : avail;
@@ -1457,17 +1603,23 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     double R = 0.0;
     bool term = false, want = false;
     if (run) {
+      OCC(OCC_ITER);
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
-      rng_phase(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
+      rng_phase<!HAS_MESH && !BVH>(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
       if (fresh) {  // main.rs:692-698
+        OCC(OCC_FRESH);
         const double tx = (double)x + gen_f64(g);
         const double u = tx / (double)(W - 1);
         const double ty = (double)y + gen_f64(g);
         const double v = 1.0 - ty / (double)(H - 1);
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
+#ifndef YART_NO_LAUNDER
+        ray = camera_ray(*kernarg_camera(), u, v, wl, g, EXT && S.has_time);
+#else
         ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
+#endif
         T = 1.0;
         depth = A.max_depth;
         fresh = false;
@@ -1475,6 +1627,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         const DevMaterial& m = S.materials[hmat];
         const uint32_t kind = m.kind;
         if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+          OCC(OCC_LAMB);
           const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
           const Onb uvw = onb_from_w(hn);
           V3 dir;
@@ -1486,9 +1639,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           } else {
             if (gen_range(g, 0.0, 1.0) < 0.5) {
               // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+              OCC(OCC_LAMB_LIGHT);
               const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
               dir = light_random(S.lights[k], hp, g);
             } else {
+              OCC(OCC_LAMB_COS);
               dir = local(uvw, random_cosine_direction(g));
             }
             const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
@@ -1520,6 +1675,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           ray.d = p;
           depth--;
         } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+          OCC(OCC_METAL);
           const V3 reflected = reflect(unit(ray.d), hn);
           V3 p;
           for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
@@ -1533,9 +1689,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           ray.d = add(reflected, smul(m.fuzz, p));
           depth--;
         } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+          OCC(OCC_DIEL);
           const double wl2 = ray.wl * ray.wl;
           const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-          const double n = sqrt(n2);
+          const double n = sqrt_x(n2);
           V3 outward;
           double ni_over_nt, cosine;
           if (dot(ray.d, hn) > 0.0) {
@@ -1548,7 +1705,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
           V3 out;
           if (disc > 0.0) {
-            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt(disc)));
+            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt_x(disc)));
             double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
             r0 = r0 * r0;
             const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
@@ -1579,6 +1736,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       } else if (want) {
+        OCC(OCC_WALK);
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       }
       if (want) {
@@ -1604,6 +1762,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
     }
     if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
+      OCC(OCC_TERM);
       double cx, cy, cz;
       cie_xyz(ray.wl, cx, cy, cz);
       double sx = cx * R, sy = cy * R, sz = cz * R;
@@ -1738,6 +1897,14 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
     case 5: out[i] = log_det(a[i]); break;
     case 6: out[i] = acos_det(a[i]); break;
     case 7: out[i] = atan2_det(a[i], b[i]); break;
+    case 8: out[i] = sqrt_x(a[i]); break;
+    case 9:  // a = n/3 vectors; out = unit(a_i)
+      if (3 * i + 2 < n) { const V3 u = unit(mk(a[3 * i], a[3 * i + 1], a[3 * i + 2])); out[3 * i] = u.x; out[3 * i + 1] = u.y; out[3 * i + 2] = u.z; }
+      break;
+    case 10: {  // a = n/3 triples over b_i > 0
+      if (3 * i + 2 < n) { double x = a[3 * i], y = a[3 * i + 1], z = a[3 * i + 2]; div3_pos(x, y, z, b[i]); out[3 * i] = x; out[3 * i + 1] = y; out[3 * i + 2] = z; }
+      break;
+    }
     default: out[i] = pow(a[i], b[i]); break;
   }
 }
@@ -1793,3 +1960,12 @@ hipError_t launch_probe_math(int op, const double* a, const double* b, uint32_t 
 }
 
 }  // namespace yart_dev
+
+#ifdef YART_OCC
+extern "C" int yart_debug_occupancy(int device, unsigned long long* out32) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(yart_dev::g_occ), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_occ), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
