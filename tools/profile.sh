@@ -21,14 +21,14 @@ step() {
 PASSES=${PASSES:-"list trace fetch write valu"}
 for p in $PASSES; do
   case $p in
-    list)  step prof_list 120 rocprofv3 -L ;;
-    trace) step prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_trace" -o run -- python3 $REPO/$PROG ;;
-    fetch) step prof_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -o run -- python3 $REPO/$PROG ;;
-    write) step prof_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/prof_write" -o run -- python3 $REPO/$PROG ;;
-    stall) step prof_stall 600 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d "$OUT/prof_stall" -o run -- python3 $REPO/$PROG ;;
-    mix)   step prof_mix 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT --output-format csv -d "$OUT/prof_mix" -o run -- python3 $REPO/$PROG ;;
-    mem)   step prof_mem 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CU_CYCLES --output-format csv -d "$OUT/prof_mem" -o run -- python3 $REPO/$PROG ;;
-    icache) step prof_icache 600 rocprofv3 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH --output-format csv -d "$OUT/prof_icache" -o run -- python3 $REPO/$PROG ;;
-    valu)  step prof_valu 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/prof_valu" -o run -- python3 $REPO/$PROG ;;
+    list)  step ${PFX:-}prof_list 120 rocprofv3 -L ;;
+    trace) step ${PFX:-}prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${PFX:-}prof_trace" -o run -- python3 $REPO/$PROG ;;
+    fetch) step ${PFX:-}prof_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/${PFX:-}prof_fetch" -o run -- python3 $REPO/$PROG ;;
+    write) step ${PFX:-}prof_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/${PFX:-}prof_write" -o run -- python3 $REPO/$PROG ;;
+    stall) step ${PFX:-}prof_stall 600 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d "$OUT/${PFX:-}prof_stall" -o run -- python3 $REPO/$PROG ;;
+    mix)   step ${PFX:-}prof_mix 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT --output-format csv -d "$OUT/${PFX:-}prof_mix" -o run -- python3 $REPO/$PROG ;;
+    mem)   step ${PFX:-}prof_mem 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INST_CYCLES_SMEM SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CU_CYCLES --output-format csv -d "$OUT/${PFX:-}prof_mem" -o run -- python3 $REPO/$PROG ;;
+    icache) step ${PFX:-}prof_icache 600 rocprofv3 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH --output-format csv -d "$OUT/${PFX:-}prof_icache" -o run -- python3 $REPO/$PROG ;;
+    valu)  step ${PFX:-}prof_valu 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/${PFX:-}prof_valu" -o run -- python3 $REPO/$PROG ;;
   esac
 done

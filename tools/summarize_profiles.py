@@ -31,12 +31,13 @@ def per_launch(pass_dir, kernel):
 def main():
     tag = sys.argv[1]
     kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<false, false, true>"
+    pfx = sys.argv[3] if len(sys.argv) > 3 else ""  # tools/profile.sh PFX= of the run
     PROF.mkdir(exist_ok=True)
-    shutil.copy(OUT / "prof_trace" / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
+    shutil.copy(OUT / (pfx + "prof_trace") / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
     summary = {"kernel": kernel, "source": "tools/profile.sh (rocprofv3 --pmc, one counter block per pass)"}
     for p in ("prof_fetch", "prof_write", "prof_valu", "prof_stall", "prof_mix", "prof_mem", "prof_icache"):
-        if (OUT / p / "run_counter_collection.csv").exists():
-            v, rows = per_launch(p, kernel)
+        if (OUT / (pfx + p) / "run_counter_collection.csv").exists():
+            v, rows = per_launch(pfx + p, kernel)
             summary.update(v)
             for r in rows:
                 if kernel in r["Kernel_Name"]:
