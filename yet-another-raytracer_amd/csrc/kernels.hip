@@ -38,24 +38,30 @@ __device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ V3 muls(V3 a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ V3 smul(double s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
-// ------------------------------------------- exact fast paths for f64 sqrt and division
+__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ V3 unit(V3 a) { double l = len(a); return mk(a.x / l, a.y / l, a.z / l); }  // vec3.rs unit_vector
+__device__ __forceinline__ V3 divs(V3 a, double s) {  // vec3.rs:109-122 (0 -> f64::MAX)
+  if (s == 0.0) return mk(kF64Max, kF64Max, kF64Max);
+  return mk(a.x / s, a.y / s, a.z / s);
+}
+
+// ------------------------------------------- exact fast cores for f64 sqrt and division
 // hipcc lowers f64 `sqrt` and `/` to IEEE-correct sequences (LLVM AMDGPU):
 //   sqrt: x < 2^-767 ? scale by 2^256 : x; v_rsq_f64; 2 Goldschmidt + 2 Newton fma steps; unscale;
 //         zero/+inf class fixup                                          (18 VALU instructions)
 //   n/d:  v_div_scale_f64 (d); v_rcp_f64; 2 Newton steps; v_div_scale_f64 (n); q = n·r;
 //         rem = fma(-d, q, n); v_div_fmas_f64 (= fma(rem, r, q) unless a scale fired);
 //         v_div_fixup_f64 (specials, sign)                                (11 VALU instructions)
-// Inside the ranges guarded below no scale step fires and the fixups pass the value through, so
-// the bare cores are bitwise the full sequences; outside them the full sequence runs. Quotients
-// sharing a positive denominator share its reciprocal (unit vectors: one chain, not three).
-// n = ±0 (which v_div_scale turns into NaN for v_div_fixup to repair) is exact in the core's
-// rem-negated form when d > 0: q = ±0·r, remn = d·q − n = +0, fma(−remn, r, q) = q.
-// Off by default (build with -DYART_FAST_MATH): measured on the MI355X, the per-operation guard
-// branches cost more than the shorter cores save (cornell 4,336 vs 4,436 Msamples/s, bitwise both).
-#if !defined(YART_FAST_MATH) && !defined(YART_SLOW_MATH)
-#define YART_SLOW_MATH
-#endif
-#ifndef YART_SLOW_MATH
+// Inside the ranges checked below no scale step fires and the fixups pass the value through, so
+// the bare cores are bitwise the full sequences. Quotients sharing a positive denominator share its
+// reciprocal chain (a unit vector: one v_rcp_f64 chain, not three). n = ±0 (which v_div_scale turns
+// into NaN for v_div_fixup to repair) is exact in the core's rem-negated form when d > 0:
+// q = ±0·r, remn = d·q − n = +0, fma(−remn, r, q) = q.
 __device__ __forceinline__ double sqrt_core(double x) {  // x in [2^-767, inf)
   const double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = y * 0.5;
@@ -79,49 +85,61 @@ __device__ __forceinline__ double div_core_pos(double n, double d, double r) {  
   const double remn = __builtin_fma(d, q, -n);
   return __builtin_fma(-remn, r, q);
 }
-// A numerator over a denominator in [2^-300, 2^300]: zero, or |n| in [2^-600, 2^400] (no scale,
-// quotient normal, exponent gap < 768).
-__device__ __forceinline__ bool num_ok(double n) { return n == 0.0 || (fabs(n) >= 0x1p-600 && fabs(n) <= 0x1p400); }
-__device__ __forceinline__ double sqrt_x(double x) {
-  if (x >= 0x1p-767 && x < INFINITY) return sqrt_core(x);
-  return sqrt(x);
-}
-#else
-__device__ __forceinline__ double sqrt_x(double x) { return sqrt(x); }
-#endif
-// n_i / s for a positive s shared by three quotients
-__device__ __forceinline__ void div3_pos(double& a, double& b, double& c, double s) {
-#ifndef YART_SLOW_MATH
-  if (s >= 0x1p-300 && s <= 0x1p300 && num_ok(a) && num_ok(b) && num_ok(c)) {
-    const double r = rcp_core(s);
-    a = div_core_pos(a, s, r); b = div_core_pos(b, s, r); c = div_core_pos(c, s, r);
-    return;
+
+// Math policies for the blocks that can run either way (scatter, closest hit). Ieee: the
+// compiler's sequences. Fast: the cores, every operand checked against its core's range with
+// compares only; a failed check sets `bad` and the caller re-runs the whole block with Ieee for
+// that lane (one rarely taken branch per block: with one branch per operation the cores lost,
+// cornell 4,336 vs 4,436 Msamples/s). Both give the same bits wherever Fast does not flag.
+struct PosDen { double d, r; };  // a positive denominator shared by several quotients
+struct Ieee {
+  static constexpr bool kFast = false;
+  __device__ __forceinline__ double sqrt(double x) { return ::sqrt(x); }
+  __device__ __forceinline__ double len(V3 a) { return ::sqrt(len2(a)); }
+  __device__ __forceinline__ V3 unit(V3 a) { return yart_dev::unit(a); }
+  __device__ __forceinline__ PosDen den(double d) { return PosDen{d, 0.0}; }
+  __device__ __forceinline__ double quo(double n, const PosDen& p) { return n / p.d; }
+};
+struct Fast {
+  static constexpr bool kFast = true;
+  bool bad = false;
+  __device__ __forceinline__ double sqrt(double x) {
+    bad |= !(x >= 0x1p-767 && x < INFINITY);
+    return sqrt_core(x);
   }
-#endif
-  a = a / s; b = b / s; c = c / s;
-}
-__device__ __forceinline__ V3 divs(V3 a, double s) {  // vec3.rs:109-122 (0 -> f64::MAX)
-  if (s == 0.0) return mk(kF64Max, kF64Max, kF64Max);
-  return mk(a.x / s, a.y / s, a.z / s);
-}
-__device__ __forceinline__ double dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
-  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ double len(V3 a) { return sqrt_x(a.x * a.x + a.y * a.y + a.z * a.z); }
-__device__ __forceinline__ V3 unit(V3 a) {  // vec3.rs unit_vector: a / |a|
-  const double l2 = a.x * a.x + a.y * a.y + a.z * a.z;
-#ifndef YART_SLOW_MATH
-  // l2 in [2^-600, 2^600] puts |a| in [2^-300, 2^300] (and its sqrt in the core's range)
-  if (l2 >= 0x1p-600 && l2 <= 0x1p600 && num_ok(a.x) && num_ok(a.y) && num_ok(a.z)) {
-    const double l = sqrt_core(l2), r = rcp_core(l);
+  __device__ __forceinline__ double len(V3 a) { return sqrt(len2(a)); }
+  __device__ __forceinline__ PosDen den(double d) {  // d in [2^-300, 2^300]
+    bad |= !(d >= 0x1p-300 && d <= 0x1p300);
+    return PosDen{d, rcp_core(d)};
+  }
+  // n = 0 or |n| in [2^-600, 2^400] over a checked denominator: no scale, normal quotient,
+  // exponent gap < 768
+  __device__ __forceinline__ double quo(double n, const PosDen& p) {
+    bad |= !(n == 0.0 || (fabs(n) >= 0x1p-600 && fabs(n) <= 0x1p400));
+    return div_core_pos(n, p.d, p.r);
+  }
+  __device__ __forceinline__ V3 unit(V3 a) {
+    // |a| in [2^-300, 2^300] (the den check) also covers the sqrt core's range: l2 tiny, zero,
+    // infinite or NaN leave l outside it. The components are at most |a|: only the lower bound.
+    const double l = sqrt_core(len2(a));
+    bad |= !(l >= 0x1p-300 && l <= 0x1p300);
+    bad |= !(a.x == 0.0 || fabs(a.x) >= 0x1p-600);
+    bad |= !(a.y == 0.0 || fabs(a.y) >= 0x1p-600);
+    bad |= !(a.z == 0.0 || fabs(a.z) >= 0x1p-600);
+    const double r = rcp_core(l);
     return mk(div_core_pos(a.x, l, r), div_core_pos(a.y, l, r), div_core_pos(a.z, l, r));
   }
+};
+__device__ __forceinline__ bool flagged(const Fast& m) { return m.bad; }
+__device__ __forceinline__ bool flagged(const Ieee&) { return false; }
+// Default Ieee. Measured with one Fast re-run branch per scatter block (bitwise either way): cornell
+// 4,421 vs 4,581 Msamples/s, random-scene 1,085 vs 1,124, david 208 vs 210 — the kept-alive inputs
+// and the second copy of the block cost more (VGPR spills 44 vs 23) than the shorter cores save.
+#ifdef YART_FAST_MATH
+typedef Fast FastMath;
+#else
+typedef Ieee FastMath;
 #endif
-  const double l = sqrt(l2);
-  return mk(a.x / l, a.y / l, a.z / l);
-}
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
 struct Ray { V3 o, d; double time, wl; };
@@ -462,7 +480,8 @@ __device__ __forceinline__ void cie_xyz(double wl, double& x, double& y, double&
 // Each primitive comes as a closest-hit test that only finds t (`*_t`) and a record builder
 // (`*_rec`) run once for the winning primitive of a world query; `*_hit` is the two together.
 // Split or not, every value is computed by the same expression on the same inputs.
-__device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {  // sphere.rs:48-86
+template <class M = Ieee>
+__device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double tmin, double tmax, double& t, M&& m = M()) {  // sphere.rs:48-86
   V3 center = mk(p[0], p[1], p[2]);
   double radius = p[3];
   V3 oc = sub(r.o, center);
@@ -471,22 +490,27 @@ __device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double t
   double c = len2(oc) - radius * radius;
   double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
-  double sq = sqrt_x(disc);
-  t = (0.0 - half_b - sq) / a;
+  double sq = m.sqrt(disc);
+  const PosDen ad = m.den(a);  // a = |d|^2 > 0 for a ray that can hit
+  t = m.quo(0.0 - half_b - sq, ad);
   if (t < tmin || tmax < t) {
-    t = (0.0 - half_b + sq) / a;
+    t = m.quo(0.0 - half_b + sq, ad);
     if (t < tmin || tmax < t) return false;
   }
   return true;
 }
-template <bool UV = false>
-__device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h) {
+template <bool UV = false, class M = Ieee>
+__device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h, M&& m = M()) {
   V3 center = mk(p[0], p[1], p[2]);
   double radius = p[3];
   V3 pt = at(r, t);
   V3 outward = sub(pt, center);  // (pt - center) / |radius| (vec3.rs:109-122: / 0 -> f64::MAX)
-  if (radius != 0.0) div3_pos(outward.x, outward.y, outward.z, fabs(radius));
-  else outward = mk(kF64Max, kF64Max, kF64Max);
+  if (radius != 0.0) {
+    const PosDen rd = m.den(fabs(radius));
+    outward = mk(m.quo(outward.x, rd), m.quo(outward.y, rd), m.quo(outward.z, rd));
+  } else {
+    outward = mk(kF64Max, kF64Max, kF64Max);
+  }
   if (radius < 0.0) { h.n = neg(outward); h.ff = dot(r.d, outward) > 0.0; }
   else { h.n = outward; h.ff = dot(r.d, outward) < 0.0; }
   h.t = t; h.p = pt;
@@ -496,10 +520,11 @@ __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double
     h.v = theta / kPi;
   }
 }
-__device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h) {
+template <class M = Ieee>
+__device__ __forceinline__ bool sphere_hit(const double* p, const Ray& r, double tmin, double tmax, Hit& h, M&& m = M()) {
   double t;
-  if (!sphere_t(p, r, tmin, tmax, t)) return false;
-  sphere_rec(p, r, t, h);
+  if (!sphere_t(p, r, tmin, tmax, t, m)) return false;
+  sphere_rec<false>(p, r, t, h, m);
   return true;
 }
 
@@ -514,7 +539,7 @@ __device__ __forceinline__ bool moving_sphere_t(const double* p, const Ray& r, d
   const double a = len2(r.d), half_b = dot(oc, r.d), c = len2(oc) - radius * radius;
   const double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
-  const double sq = sqrt_x(disc);
+  const double sq = sqrt(disc);
   t = (0.0 - half_b - sq) / a;
   if (t < tmin || tmax < t) {
     t = (0.0 - half_b + sq) / a;
@@ -1232,30 +1257,33 @@ __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ra
 
 // ----------------------------------------------------------------------- ONB and PDFs
 struct Onb { V3 u, v, w; };
-__device__ __forceinline__ Onb onb_from_w(V3 n) {  // onb.rs:10-21
+template <class M>
+__device__ __forceinline__ Onb onb_from_w(V3 n, M& m) {  // onb.rs:10-21
   Onb b;
-  b.w = unit(n);
+  b.w = m.unit(n);
   const V3 a = fabs(b.w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
-  b.v = unit(cross(b.w, a));
+  b.v = m.unit(cross(b.w, a));
   b.u = cross(b.w, b.v);
   return b;
 }
 __device__ __forceinline__ V3 local(const Onb& b, V3 a) { return add(add(smul(a.x, b.u), smul(a.y, b.v)), smul(a.z, b.w)); }
-__device__ __forceinline__ V3 random_cosine_direction(Rng& g) {  // pdf.rs:15-25
+template <class M>
+__device__ __forceinline__ V3 random_cosine_direction(Rng& g, M& m) {  // pdf.rs:15-25
   const double r1 = gen_f64(g), r2 = gen_f64(g);
-  const double z = sqrt_x(1.0 - r2);
+  const double z = m.sqrt(1.0 - r2);
   double s, c;
   sincos_det(2.0 * kPi * r1, s, c);
-  const double sr2 = sqrt_x(r2);
+  const double sr2 = m.sqrt(r2);
   return mk(c * sr2, s * sr2, z);
 }
-__device__ __forceinline__ double cosine_value(const Onb& b, V3 d) {  // pdf.rs:40-47
-  const double cosine = dot(unit(d), b.w);
+template <class M>
+__device__ __forceinline__ double cosine_value(const Onb& b, V3 d, M& m) {  // pdf.rs:40-47
+  const double cosine = dot(m.unit(d), b.w);
   return cosine <= 0.0 ? 0.0 : cosine / kPi;
 }
 
-template <bool STATS>
-__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st) {
+template <bool STATS, class M>
+__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st, M& m) {
   if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
   Ray r{origin, dir, 0.0, wl};
   Hit h;
@@ -1264,20 +1292,21 @@ __device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 di
     if (!xz_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
     const double area = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
     const double distance_squared = h.t * h.t * len2(dir);
-    const double cosine = fabs(dot(dir, h.n)) / len(dir);
+    const double cosine = fabs(dot(dir, h.n)) / m.len(dir);
     return distance_squared / (cosine * area);
   }
   if (o.kind == YART_PRIM_SPHERE) {  // sphere.rs:95-110
     if (STATS) st.v[ST_LIGHT]++;
-    if (!sphere_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
+    if (!sphere_hit(o.p, r, 0.001, INFINITY, h, m)) return 0.0;
     const double radius = o.p[3];
-    const double cos_theta_max = sqrt_x(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
+    const double cos_theta_max = m.sqrt(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
     const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
     return 1.0 / solid_angle;
   }
   return 0.0;
 }
-__device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g) {
+template <class M>
+__device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g, M& m) {
   if (o.n_xf == 0 && o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:164-171
     const double x = gen_range(g, o.p[0], o.p[1]);
     const double z = gen_range(g, o.p[2], o.p[3]);
@@ -1286,13 +1315,13 @@ __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g
   if (o.n_xf == 0 && o.kind == YART_PRIM_SPHERE) {  // sphere.rs:112-118, 11-21
     const V3 direction = sub(ld3(o.p), origin);
     const double d2 = len2(direction);
-    const Onb uvw = onb_from_w(direction);
+    const Onb uvw = onb_from_w(direction, m);
     const double r1 = gen_f64(g), r2 = gen_f64(g);
     const double radius = o.p[3];
-    const double z = 1.0 + r2 * (sqrt_x(1.0 - radius * radius / d2) - 1.0);
+    const double z = 1.0 + r2 * (m.sqrt(1.0 - radius * radius / d2) - 1.0);
     double s, c;
     sincos_det(2.0 * kPi * r1, s, c);
-    const double sz = sqrt_x(1.0 - z * z);
+    const double sz = m.sqrt(1.0 - z * z);
     const V3 rs = mk(c * sz, s * sz, z);
     return local(uvw, rs);
   }
@@ -1624,100 +1653,119 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         depth = A.max_depth;
         fresh = false;
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
-        const DevMaterial& m = S.materials[hmat];
-        const uint32_t kind = m.kind;
-        if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-          OCC(OCC_LAMB);
-          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-          const Onb uvw = onb_from_w(hn);
-          V3 dir;
-          double pdf_val;
-          if (S.n_lights == 0) {
-            (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
-            dir = local(uvw, random_cosine_direction(g));
-            pdf_val = 0.5 * cosine_value(uvw, dir) + 0.5 * cosine_value(uvw, dir);
-          } else {
-            if (gen_range(g, 0.0, 1.0) < 0.5) {
-              // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
-              OCC(OCC_LAMB_LIGHT);
-              const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
-              dir = light_random(S.lights[k], hp, g);
+        // One body, two math policies: the Fast cores first; a lane with an operand outside a
+        // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
+        auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_) {
+          T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false;
+          const DevMaterial& m = S.materials[hmat];
+          const uint32_t kind = m.kind;
+          if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+            OCC(OCC_LAMB);
+            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            const Onb uvw = onb_from_w(hn, mp);
+            V3 dir;
+            double pdf_val;
+            if (S.n_lights == 0) {
+              (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
+              dir = local(uvw, random_cosine_direction(g, mp));
+              pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
             } else {
-              OCC(OCC_LAMB_COS);
-              dir = local(uvw, random_cosine_direction(g));
+              if (gen_range(g, 0.0, 1.0) < 0.5) {
+                // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+                OCC(OCC_LAMB_LIGHT);
+                const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+                dir = light_random(S.lights[k], hp, g, mp);
+              } else {
+                OCC(OCC_LAMB_COS);
+                dir = local(uvw, random_cosine_direction(g, mp));
+              }
+              const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+              double sum = -0.0;
+              for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
+              pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
             }
-            const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-            double sum = -0.0;
-            for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st);
-            pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir);
+            if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+              R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+              term_ = true;
+            } else {
+              const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+              const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+              T_ = ((T * att) * spdf) / pdf_val;
+              o_ = hp;
+              d_ = dir;
+              depth_ = depth - 1;
+            }
+          } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
+            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            V3 p;
+            for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+              const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+              p = mk(px, py, pz);
+              if (!(len2(p) >= 1.0)) break;
+            }
+            T_ = T * att;
+            o_ = hp;
+            d_ = p;
+            depth_ = depth - 1;
+          } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+            OCC(OCC_METAL);
+            const V3 reflected = reflect(mp.unit(ray.d), hn);
+            V3 p;
+            for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+              const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+              p = mk(px, py, pz);
+              if (!(len2(p) >= 1.0)) break;
+            }
+            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            T_ = T * att;
+            o_ = hp;
+            d_ = add(reflected, smul(m.fuzz, p));
+            depth_ = depth - 1;
+          } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+            OCC(OCC_DIEL);
+            const double wl2 = ray.wl * ray.wl;
+            const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+            const double n = mp.sqrt(n2);
+            // |d| divides the incidence cosine and, in unit_vector(d), the three components
+            const PosDen ld = mp.den(mp.len(ray.d));
+            V3 outward;
+            double ni_over_nt, cosine;
+            if (dot(ray.d, hn) > 0.0) {
+              outward = neg(hn); ni_over_nt = n; cosine = mp.quo(n * dot(ray.d, hn), ld);
+            } else {
+              outward = hn; ni_over_nt = 1.0 / n; cosine = mp.quo(-dot(ray.d, hn), ld);
+            }
+            const V3 uv = mk(mp.quo(ray.d.x, ld), mp.quo(ray.d.y, ld), mp.quo(ray.d.z, ld));  // refract (material.rs:195-205)
+            const double dt = dot(uv, outward);
+            const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+            V3 out;
+            if (disc > 0.0) {
+              const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, mp.sqrt(disc)));
+              double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+              r0 = r0 * r0;
+              const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+              out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
+            } else {
+              out = reflect(ray.d, hn);
+            }
+            T_ = T * 1.0;
+            o_ = hp;
+            d_ = out;
+            depth_ = depth - 1;
           }
-          if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-            R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-            term = true;
-          } else {
-            const double cosine = dot(hn, unit(dir));  // Lambertian::scatter_pdf
-            const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-            T = ((T * att) * spdf) / pdf_val;
-            ray.o = hp;
-            ray.d = dir;
-            depth--;
-          }
-        } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-          V3 p;
-          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-            p = mk(px, py, pz);
-            if (!(len2(p) >= 1.0)) break;
-          }
-          T = T * att;
-          ray.o = hp;
-          ray.d = p;
-          depth--;
-        } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
-          OCC(OCC_METAL);
-          const V3 reflected = reflect(unit(ray.d), hn);
-          V3 p;
-          for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-            const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-            p = mk(px, py, pz);
-            if (!(len2(p) >= 1.0)) break;
-          }
-          const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
-          T = T * att;
-          ray.o = hp;
-          ray.d = add(reflected, smul(m.fuzz, p));
-          depth--;
-        } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
-          OCC(OCC_DIEL);
-          const double wl2 = ray.wl * ray.wl;
-          const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-          const double n = sqrt_x(n2);
-          V3 outward;
-          double ni_over_nt, cosine;
-          if (dot(ray.d, hn) > 0.0) {
-            outward = neg(hn); ni_over_nt = n; cosine = n * dot(ray.d, hn) / len(ray.d);
-          } else {
-            outward = hn; ni_over_nt = 1.0 / n; cosine = -dot(ray.d, hn) / len(ray.d);
-          }
-          const V3 uv = unit(ray.d);  // refract (material.rs:195-205)
-          const double dt = dot(uv, outward);
-          const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
-          V3 out;
-          if (disc > 0.0) {
-            const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, sqrt_x(disc)));
-            double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
-            r0 = r0 * r0;
-            const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
-            out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
-          } else {
-            out = reflect(ray.d, hn);
-          }
-          T = T * 1.0;
-          ray.o = hp;
-          ray.d = out;
-          depth--;
+        };
+        double nT, nR;
+        V3 no, nd;
+        uint32_t ndepth;
+        bool nterm;
+        FastMath fm;
+        scatter(fm, nT, no, nd, ndepth, nR, nterm);
+        if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
+          rng_phase<!HAS_MESH && !BVH>(g, pixel, smp, A.max_depth - depth + 1u);
+          Ieee im;
+          scatter(im, nT, no, nd, ndepth, nR, nterm);
         }
+        T = nT; ray.o = no; ray.d = nd; depth = ndepth; R = nR; term = nterm;
       }
       if (!term) {
         if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
@@ -1897,12 +1945,27 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
     case 5: out[i] = log_det(a[i]); break;
     case 6: out[i] = acos_det(a[i]); break;
     case 7: out[i] = atan2_det(a[i], b[i]); break;
-    case 8: out[i] = sqrt_x(a[i]); break;
+    // 8-10: the Fast policy's cores where its checks pass, the IEEE sequence where they flag —
+    // what a Fast block followed by its Ieee re-run produces
+    case 8: { Fast m; const double v = m.sqrt(a[i]); out[i] = m.bad ? sqrt(a[i]) : v; break; }
     case 9:  // a = n/3 vectors; out = unit(a_i)
-      if (3 * i + 2 < n) { const V3 u = unit(mk(a[3 * i], a[3 * i + 1], a[3 * i + 2])); out[3 * i] = u.x; out[3 * i + 1] = u.y; out[3 * i + 2] = u.z; }
+      if (3 * i + 2 < n) {
+        const V3 in = mk(a[3 * i], a[3 * i + 1], a[3 * i + 2]);
+        Fast m;
+        V3 u = m.unit(in);
+        if (m.bad) u = unit(in);
+        out[3 * i] = u.x; out[3 * i + 1] = u.y; out[3 * i + 2] = u.z;
+      }
       break;
     case 10: {  // a = n/3 triples over b_i > 0
-      if (3 * i + 2 < n) { double x = a[3 * i], y = a[3 * i + 1], z = a[3 * i + 2]; div3_pos(x, y, z, b[i]); out[3 * i] = x; out[3 * i + 1] = y; out[3 * i + 2] = z; }
+      if (3 * i + 2 < n) {
+        Fast m;
+        const PosDen d = m.den(b[i]);
+        const double x = m.quo(a[3 * i], d), y = m.quo(a[3 * i + 1], d), z = m.quo(a[3 * i + 2], d);
+        out[3 * i] = m.bad ? a[3 * i] / b[i] : x;
+        out[3 * i + 1] = m.bad ? a[3 * i + 1] / b[i] : y;
+        out[3 * i + 2] = m.bad ? a[3 * i + 2] / b[i] : z;
+      }
       break;
     }
     default: out[i] = pow(a[i], b[i]); break;
