@@ -3,8 +3,9 @@
 Metric: Msamples/s (W x H x spp / s) for cornell-box 800x800, 256 spp, depth 50 (configs[1]);
 ms_per_step is the wall-clock of one frame. A step = one frame of the hot path: every rank
 renders its share of 8x8-pixel blocks (block b -> rank b % N) with the HIP megakernel through the
-C ABI (yart_render_async), the shards are summed into rank 0's frame with ONE RCCL reduce over
-xGMI (N > 1), and rank 0 runs finalize (XYZ -> sRGB RGBA8). Inputs (scene, BVH, camera) are
+C ABI (yart_render_async), each rank's pixels are collected into rank 0's frame with ONE RCCL
+gather over xGMI (N > 1; yart.shard.ShardGather), and rank 0 runs finalize (XYZ -> sRGB RGBA8).
+Inputs (scene, BVH, camera) are
 resident in HBM before the timed region. Scaling is strong: the frame is fixed as N grows.
 
 Also reported on the same line:
@@ -31,7 +32,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
 import yart  # noqa: E402
-from yart.shard import assemble_frame  # noqa: E402
+from yart.shard import ShardGather, assemble_frame  # noqa: E402
 
 WORKLOAD = dict(scene="cornell-box", width=800, height=800, spp=256, max_depth=50)
 
@@ -100,8 +101,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N>1 path on a 1-GPU box (RCCL refuses two ranks on one device): every rank on
+    # device 0, the collective over gloo on host copies. Never set for a real run.
+    rehearse = os.environ.get("YART_BENCH_SAME_DEVICE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     W, H, spp, depth = WORKLOAD["width"], WORKLOAD["height"], WORKLOAD["spp"], WORKLOAD["max_depth"]
@@ -112,15 +121,32 @@ def main():
     scene = yart.DeviceScene(preset.desc, device=local)
     mine = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)   # this rank's blocks, zeros elsewhere
     frame = torch.zeros_like(mine) if world > 1 else mine
+    gather = ShardGather(W, H, 3, world, rank, torch.device("cpu") if rehearse else dev) if world > 1 else None
+    if rehearse and world > 1:
+        mine_h, frame_h = torch.zeros_like(mine, device="cpu"), torch.zeros_like(frame, device="cpu")
     rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     L = yart.load_device()
+
+    collective = ["gather"]
 
     def step():
         # render kernel(s) bracketed by HIP events the library records on this stream
         scene.render_async(cam, prm, mine.data_ptr(), stream.cuda_stream)
         if world > 1:
-            assemble_frame(mine, frame, dist, dst=0)
+            if rehearse:
+                mine_h.copy_(mine)
+                gather(mine_h, frame_h, dist)
+                frame.copy_(frame_h)
+            elif collective[0] == "gather":
+                try:
+                    gather(mine, frame, dist)  # each rank's own pixels -> rank 0's frame (one gather)
+                except RuntimeError as e:  # a backend without gather: the full-frame reduce instead
+                    print(f"rank {rank}: gather failed ({e}); using reduce", file=sys.stderr, flush=True)
+                    collective[0] = "reduce"
+                    assemble_frame(mine, frame, dist, dst=0)
+            else:
+                assemble_frame(mine, frame, dist, dst=0)
         if rank == 0:
             rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
                                              yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(stream.cuda_stream))
@@ -141,7 +167,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     render_ms, accum_ms, frames = scene.frame_timing(stream.cuda_stream)
@@ -152,6 +178,12 @@ def main():
     if rank == 0:
         f = frame.float()
         assert torch.isfinite(f).all() and f.abs().sum() > 0
+        if rehearse and world > 1:  # the assembled shards are bitwise the one-rank frame
+            full = torch.zeros_like(mine)
+            scene.render_async(cam, yart.render_params(W, H, spp, depth), full.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            assert torch.equal(full, frame), "sharded frame differs from the one-rank render"
+            print("rehearsal: sharded frame bitwise equal to the one-rank render", flush=True)
 
     roofline = None
     cpu = None
@@ -185,6 +217,7 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
             "config": {"workload": "cornell-box 800x800x256spp depth 50 (BASELINE configs[1])", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"pixel-blocks x{world}",
+                       "collective": (collective[0] + (" (gloo rehearsal)" if rehearse else " (RCCL)")) if world > 1 else None,
                        "seed": yart.DEFAULT_SEED},
             "roofline": roofline, "cpu_baseline": cpu,
         }

@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 
 import oracle_lib as O
 import yart
-from yart.shard import assemble_frame, block_owner
+from yart.shard import ShardGather, assemble_frame, block_owner
 
 W, H, SPP, DEPTH = 40, 24, 2, 50
 
@@ -40,6 +40,16 @@ def _worker(rank, world, port, out_path):
         assemble_frame(mine, frame, dist, dst=0)
     if rank == 0:
         np.save(out_path, frame.numpy())
+    # bench.py's path: each rank's own pixels, one gather; the non-owned part of `mine` is garbage
+    # here to show it is never read
+    mine2 = mine.clone()
+    mine2[torch.from_numpy(block_owner(W, H, world) != rank)] = float("nan")
+    g = ShardGather(W, H, 3, world, rank, torch.device("cpu"))
+    frame2 = torch.full_like(mine, -1.0)
+    for _ in range(2):
+        g(mine2, frame2, dist)
+    if rank == 0:
+        np.save(out_path.replace(".npy", "_gather.npy"), frame2.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -51,6 +61,7 @@ def test_two_rank_gloo_frame_assembly(tmp_path, world):
     p = yart.Preset("cornell-box")
     full = O.OracleScene(p.desc).render(p.camera(W, H), yart.render_params(W, H, SPP, DEPTH), threads=2)
     np.testing.assert_array_equal(np.load(out), full)
+    np.testing.assert_array_equal(np.load(str(out).replace(".npy", "_gather.npy")), full)
 
 
 def test_block_owner_matches_shard_renders():
