@@ -30,13 +30,21 @@ static void mkdirs(const std::string& d) {
   }
 }
 
+static const char kUsage[] =
+    "Usage: yart --scene <SCENE> [--output <OUTPUT>] [--width <WIDTH>] [--height <HEIGHT>] "
+    "[--samples <SAMPLES>] [--max-depth <MAX_DEPTH>] [--workers <WORKERS>] [--vfov <VFOV>] "
+    "[--aperture <APERTURE>] [--seed <SEED>] [--gpus <GPUS>] [--assets <DIR>]\n";
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i) {  // clap's -h / --help (main.rs:78-107 derives Parser)
+    if (std::strcmp(argv[i], "-h") == 0 || std::strcmp(argv[i], "--help") == 0) {
+      std::fputs(kUsage, stdout);
+      return 0;
+    }
+  }
   yart_cli cli;
   if (yart_cli_parse(argc, (const char* const*)argv, &cli) != YART_OK) {
-    std::fprintf(stderr, "error: %s\n\nUsage: yart --scene <SCENE> [--output <OUTPUT>] [--width <WIDTH>] [--height <HEIGHT>] "
-                         "[--samples <SAMPLES>] [--max-depth <MAX_DEPTH>] [--workers <WORKERS>] [--vfov <VFOV>] "
-                         "[--aperture <APERTURE>] [--seed <SEED>] [--gpus <GPUS>] [--assets <DIR>]\n",
-                 yart_host_last_error());
+    std::fprintf(stderr, "error: %s\n\n%s", yart_host_last_error(), kUsage);
     return 2;
   }
   std::string assets = cli.assets[0] ? cli.assets : "assets";
