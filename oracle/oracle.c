@@ -335,17 +335,75 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-typedef struct { uint32_t key[2]; uint32_t ctr[4]; uint32_t buf[4]; int have; } rng_t;
+/* Independent-stream mode (oracle_render mode bit 2, statistical tests only): the reference's own
+ * generator family — rand 0.8.5's ThreadRng is ChaCha12 (rand_chacha 0.3: 12 rounds, 64-bit block
+ * counter in words 12-13, next_u64 = two consecutive u32 words, low first) — one sequential stream
+ * per (seed, pixel, sample) with the key drawn by splitmix64, no phases: every draw of the path in
+ * the reference's order, rejection loops included. Its images must agree with the Philox ones in
+ * distribution (tests/test_statistical.py), not in bits. */
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+#define CHACHA_QR(a, b, c, d)                        \
+  a += b; d ^= a; d = rotl32(d, 16);                 \
+  c += d; b ^= c; b = rotl32(b, 12);                 \
+  a += b; d ^= a; d = rotl32(d, 8);                  \
+  c += d; b ^= c; b = rotl32(b, 7);
+void oracle_chacha_block(const uint32_t in[16], uint32_t out[16], int double_rounds) {
+  uint32_t x[16];
+  memcpy(x, in, sizeof x);
+  for (int i = 0; i < double_rounds; ++i) {
+    CHACHA_QR(x[0], x[4], x[8], x[12]) CHACHA_QR(x[1], x[5], x[9], x[13])
+    CHACHA_QR(x[2], x[6], x[10], x[14]) CHACHA_QR(x[3], x[7], x[11], x[15])
+    CHACHA_QR(x[0], x[5], x[10], x[15]) CHACHA_QR(x[1], x[6], x[11], x[12])
+    CHACHA_QR(x[2], x[7], x[8], x[13]) CHACHA_QR(x[3], x[4], x[9], x[14])
+  }
+  for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+void oracle_chacha12_block(const uint32_t in[16], uint32_t out[16]) { oracle_chacha_block(in, out, 6); }
+static inline uint64_t splitmix64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+typedef struct {
+  uint32_t key[2]; uint32_t ctr[4]; uint32_t buf[4]; int have;
+  int chacha; uint32_t cc_in[16]; uint32_t cc_out[16]; int cc_have;
+} rng_t;
 static void rng_init(rng_t* r, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
   r->key[0] = (uint32_t)seed; r->key[1] = (uint32_t)(seed >> 32);
   r->ctr[0] = 0; r->ctr[1] = sample; r->ctr[2] = pixel; r->ctr[3] = stream;
   r->have = 0;
+  r->chacha = 0;
+}
+static void rng_init_chacha(rng_t* r, uint64_t seed, uint32_t pixel, uint32_t sample) {
+  static const uint32_t sigma[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+  rng_init(r, seed, pixel, sample, 0);
+  r->chacha = 1;
+  uint64_t sm = seed ^ (((uint64_t)pixel << 32) | sample) * 0xD1342543DE82EF95ull;
+  memcpy(r->cc_in, sigma, sizeof sigma);
+  for (int i = 0; i < 4; ++i) {
+    uint64_t k = splitmix64(&sm);
+    r->cc_in[4 + 2 * i] = (uint32_t)k; r->cc_in[5 + 2 * i] = (uint32_t)(k >> 32);
+  }
+  r->cc_in[12] = r->cc_in[13] = r->cc_in[14] = r->cc_in[15] = 0;
+  r->cc_have = 0;
 }
 static void rng_phase(rng_t* r, uint32_t phase) {
+  if (r->chacha) return; /* one sequential stream, as thread_rng */
   r->ctr[0] = 0; r->ctr[3] = (phase << 2) | (r->ctr[3] & 3u);
   r->have = 0;
 }
 static inline uint64_t rng_u64(rng_t* r) {
+  if (r->chacha) {
+    if (r->cc_have < 2) { /* a u64 never straddles blocks: 16 words = 8 draws */
+      oracle_chacha12_block(r->cc_in, r->cc_out);
+      if (++r->cc_in[12] == 0) ++r->cc_in[13];
+      r->cc_have = 16;
+    }
+    int i = 16 - r->cc_have; r->cc_have -= 2;
+    return ((uint64_t)r->cc_out[i + 1] << 32) | r->cc_out[i];
+  }
   if (r->have == 0) { oracle_philox4x32_10(r->ctr, r->key, r->buf); r->ctr[0]++; r->have = 2; }
   int i = 2 - r->have; r->have--;
   return ((uint64_t)r->buf[2 * i + 1] << 32) | r->buf[2 * i];
@@ -1275,7 +1333,7 @@ int oracle_coverage(uint32_t w, uint32_t h, uint8_t* mask) {
 
 typedef struct {
   const oracle_scene* s; const yart_camera* cam; const yart_render_params* p;
-  double* out; const uint8_t* cx; const uint8_t* cy; int mode;
+  double* out; const uint8_t* cx; const uint8_t* cy; int mode; int chacha;
   volatile int next_row; pthread_mutex_t mu;
 } job_t;
 
@@ -1285,7 +1343,9 @@ static void render_pixel(const job_t* j, uint32_t x, uint32_t y) {
   uint32_t pixel = y * W + x;
   double acc[3] = {0.0, 0.0, 0.0};
   for (uint32_t smp = 0; smp < p->spp; ++smp) { /* main.rs:691-708 */
-    rng_t g; rng_init(&g, p->seed, pixel, smp, 0);
+    rng_t g;
+    if (j->chacha) rng_init_chacha(&g, p->seed, pixel, smp);
+    else rng_init(&g, p->seed, pixel, smp, 0);
     double tx = (double)x + gen_f64(&g);
     double u = tx / (double)(W - 1);
     double ty = (double)y + gen_f64(&g);
@@ -1332,7 +1392,7 @@ int oracle_render(const oracle_scene* s, const yart_camera* cam, const yart_rend
   if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
   if (threads < 1) threads = 1;
   job_t j;
-  j.s = s; j.cam = cam; j.p = p; j.out = xyz_sum; j.mode = mode; j.next_row = 0;
+  j.s = s; j.cam = cam; j.p = p; j.out = xyz_sum; j.mode = mode & 1; j.chacha = (mode & 2) != 0; j.next_row = 0;
   uint8_t* cx = (uint8_t*)malloc(p->width); uint8_t* cy = (uint8_t*)malloc(p->height);
   coverage_axes(p->width, p->height, cx, cy);
   j.cx = cx; j.cy = cy;

@@ -36,10 +36,13 @@ int oracle_qbvh_stats(const oracle_scene* s, uint32_t m, uint32_t* nodes, uint32
                       uint32_t* depth);
 
 /* main.rs:628-760 with the shared counter RNG. mode 0 = iterative reflectance (the form the
- * device uses), 1 = literal recursion (main.rs:537-588). xyz_sum: W*H*3, only this shard's
- * covered pixels are written. threads <= 0: use all online CPUs. */
+ * device uses), 1 = literal recursion (main.rs:537-588); | 2 = independent-stream mode (ChaCha12,
+ * the reference's generator family, one sequential stream per sample; statistical tests only).
+ * xyz_sum: W*H*3, only this shard's covered pixels are written. threads <= 0: all online CPUs. */
 int oracle_render(const oracle_scene* s, const yart_camera* cam, const yart_render_params* p,
                   double* xyz_sum, int threads, int mode);
+void oracle_chacha_block(const uint32_t in[16], uint32_t out[16], int double_rounds);
+void oracle_chacha12_block(const uint32_t in[16], uint32_t out[16]);
 /* main.rs:710-718 finalize. */
 int oracle_finalize_rgba8(const double* xyz_sum, uint32_t w, uint32_t h, uint32_t spp,
                           uint8_t* rgba);

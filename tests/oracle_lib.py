@@ -77,9 +77,10 @@ class OracleScene:
         assert rc == 0
         return n.value, l.value, d.value
 
-    def render(self, cam, params, threads=0, recursive=False):
+    def render(self, cam, params, threads=0, recursive=False, chacha=False):
         out = np.zeros((params.height, params.width, 3), dtype=np.float64)
-        rc = lib().oracle_render(self._s, C.byref(cam), C.byref(params), _p(out), threads, 1 if recursive else 0)
+        rc = lib().oracle_render(self._s, C.byref(cam), C.byref(params), _p(out), threads,
+                                  (1 if recursive else 0) | (2 if chacha else 0))
         assert rc == 0
         return out
 
