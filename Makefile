@@ -34,7 +34,7 @@ $(LIB)/libyart_host.so: $(HOST_SRCS) $(HOST_HDRS)
 
 $(LIB)/libyart.so: $(DEV_SRCS) $(DEV_HDRS) $(GEN)/cie_xyz.inc $(GEN)/smits.inc
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(DEV_SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(DEV_SRCS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(BIN)/yart: $(PKG)/host/main.cpp $(LIB)/libyart.so $(LIB)/libyart_host.so
 	@mkdir -p $(BIN)
@@ -48,5 +48,5 @@ clean:
 # A/B builds for tools/ab.py: make variant NAME=x DEFS="-DYART_FOO"
 variant: $(GEN)/cie_xyz.inc $(GEN)/smits.inc
 	@mkdir -p $(LIB)/variants
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIB)/variants/libyart_$(NAME).so $(DEV_SRCS)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIB)/variants/libyart_$(NAME).so $(DEV_SRCS) -L/opt/rocm/lib -lrccl
 .PHONY: variant

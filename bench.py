@@ -3,23 +3,29 @@
 Metric: Msamples/s (W x H x spp / s) for cornell-box 800x800, 256 spp, depth 50 (configs[1]);
 ms_per_step is the wall-clock of one frame. A step = one frame of the hot path: every rank
 renders its share of 8x8-pixel blocks (block b -> rank b % N) with the HIP megakernel through the
-C ABI (yart_render_async), each rank's pixels are collected into rank 0's frame with ONE RCCL
-gather over xGMI (N > 1; yart.shard.ShardGather), and rank 0 runs finalize (XYZ -> sRGB RGBA8).
-Inputs (scene, BVH, camera) are
-resident in HBM before the timed region. Scaling is strong: the frame is fixed as N grows.
+C ABI, and rank 0 finalizes the frame (XYZ -> sRGB RGBA8). For N > 1 each rank renders straight
+into its block-packed shard (yart_render_packed_async) and ONE RCCL gather over xGMI issued by
+libyart itself (yart_gather_frame_async: ncclGather + an unpack kernel on rank 0) assembles rank
+0's frame; torch.distributed (gloo) is only the control plane (the communicator id, barriers, the
+max-over-ranks time). Inputs (scene, BVH, camera) are resident in HBM before the timed region.
+Scaling is strong: the frame is fixed as N grows.
 
 Also reported on the same line:
-  roofline      the render kernel's average launch duration (HIP events on the stream it runs on)
-                against the f64 VALU peak, with algorithmic FLOPs from the kernel's own work
-                counters (an untimed instrumented launch of the same frame) x the per-operation
-                FLOP model in DESIGN.md; HBM traffic from the committed rocprofv3 PMC summary.
+  roofline      the render kernel's average launch duration (HIP events the library records on
+                the stream it launches on) against the f64 VALU peak, with ALGORITHMIC FLOPs =
+                the kernel's own work counters (an untimed instrumented launch of the same frame)
+                x the per-operation FLOP model in DESIGN.md ("achieved_kind": modelled, not a
+                counter reading); HBM traffic from the committed rocprofv3 PMC snapshot, reported
+                only while it belongs to the current kernel source (sha256 of csrc/kernels.hip).
   cpu_baseline  the CPU restatement (oracle/) on this host's cores, rank 0 only, on a bounded
-                sample of the same workload (same frame at fewer spp; Msamples/s is ~spp-invariant).
+                sample of the same workload (same frame at fewer spp; Msamples/s is ~spp-invariant),
+                with the host's nproc, usable CPUs and CPU model.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -32,7 +38,7 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
 import yart  # noqa: E402
-from yart.shard import ShardGather, assemble_frame  # noqa: E402
+from yart.shard import PackedGather  # noqa: E402
 
 WORKLOAD = dict(scene="cornell-box", width=800, height=800, spp=256, max_depth=50)
 
@@ -55,15 +61,41 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-spp", type=int, default=128, help="spp of the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the CPU baseline (0 = the CPUs this process may use, at most 16: "
+                         "the GPU box's share per GPU)")
     ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
     ap.add_argument("--spu", type=int, default=0, help="samples per work unit (0 = library's choice)")
     return ap.parse_args()
 
 
+def host_cpus():
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:  # cgroup v2 CPU quota, if any ("max 100000" = none)
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except Exception:
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"nproc": os.cpu_count(), "usable": usable, "cgroup_quota": quota, "model": model}
+
+
 def cpu_baseline(preset, cam, w, h, spp, depth, threads):
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
+    hc = host_cpus()
+    if threads <= 0:
+        threads = min(16, hc["usable"], int(hc["cgroup_quota"]) if hc["cgroup_quota"] else 1 << 30)
+        threads = max(1, threads)
     scene = O.OracleScene(preset.desc)
     prm = yart.render_params(w, h, spp, depth)
     t0 = time.perf_counter()
@@ -71,18 +103,27 @@ def cpu_baseline(preset, cam, w, h, spp, depth, threads):
     dt = time.perf_counter() - t0
     return {"value": round(w * h * spp / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{WORKLOAD['scene']} {w}x{h}x{spp}spp depth {depth} (full frame, reduced spp), "
-                      f"{dt:.2f} s on {threads} threads, oracle/ C restatement"}
+                      f"{dt:.2f} s on {threads} threads, oracle/ C restatement (reference-semantics, not the Rust binary)",
+            "host": hc}
 
 
-def pmc_summary():
-    """The committed rocprofv3 PMC summary of the render kernel (tools/profile.sh), if present."""
+def kernels_sha256():
+    return hashlib.sha256((ROOT / "yet-another-raytracer_amd" / "csrc" / "kernels.hip").read_bytes()).hexdigest()
+
+
+def pmc_snapshot():
+    """The committed rocprofv3 PMC summary of the render kernel (tools/profile.sh +
+    tools/summarize_profiles.py), if it was taken on the current kernel source."""
     p = ROOT / "profiles" / "pmc_render_cornell.json"
     if not p.exists():
-        return {}
+        return {}, "no profile"
     try:
-        return json.loads(p.read_text())
+        pmc = json.loads(p.read_text())
     except Exception:
-        return {}
+        return {}, "unreadable profile"
+    if pmc.get("kernels_sha256") != kernels_sha256():
+        return {}, "stale: profiles/pmc_render_cornell.json was taken on another kernels.hip"
+    return pmc, "profiles/pmc_render_cornell.json (rocprofv3 --pmc snapshot of this kernel source)"
 
 
 def valu_issue(pmc):
@@ -102,15 +143,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal of the N>1 path on a 1-GPU box (RCCL refuses two ranks on one device): every rank on
-    # device 0, the collective over gloo on host copies. Never set for a real run.
+    # device 0, the packed shards gathered over gloo on host copies. Never set for a real run.
     rehearse = os.environ.get("YART_BENCH_SAME_DEVICE") == "1"
     if rehearse:
         local = 0
     if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")  # control plane only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     W, H, spp, depth = WORKLOAD["width"], WORKLOAD["height"], WORKLOAD["spp"], WORKLOAD["max_depth"]
@@ -119,34 +157,54 @@ def main():
     cam = preset.camera(W, H)
     prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world, samples_per_unit=a.spu)
     scene = yart.DeviceScene(preset.desc, device=local)
-    mine = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)   # this rank's blocks, zeros elsewhere
-    frame = torch.zeros_like(mine) if world > 1 else mine
-    gather = ShardGather(W, H, 3, world, rank, torch.device("cpu") if rehearse else dev) if world > 1 else None
-    if rehearse and world > 1:
-        mine_h, frame_h = torch.zeros_like(mine, device="cpu"), torch.zeros_like(frame, device="cpu")
+    frame = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)  # rank 0: the assembled frame
     rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     L = yart.load_device()
 
-    collective = ["gather"]
+    # N > 1: the data-plane collective, chosen ONCE and identically on every rank
+    collective, comm, gather, nccl_group = None, None, None, None
+    if world > 1:
+        packed = torch.zeros(yart.shard_packed_len(W, H, 0, world), dtype=torch.float64, device=dev)
+        if rehearse:
+            collective = "gather (gloo rehearsal, host copies)"
+            packed_h, frame_h = torch.zeros_like(packed, device="cpu"), torch.zeros_like(frame, device="cpu")
+            gather = PackedGather(W, H, world, rank, torch.device("cpu"))
+        else:
+            uid = [yart.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            ok = 1
+            try:
+                comm = yart.Comm(uid[0], world, rank, local)
+            except yart.YartError as e:
+                print(f"rank {rank}: libyart RCCL communicator failed ({e})", file=sys.stderr, flush=True)
+                ok = 0
+            t = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if t.item():
+                collective = "ncclGather (libyart yart_gather_frame_async, RCCL)"
+            else:  # the same packets through torch's RCCL process group
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                nccl_group = dist.new_group(backend="nccl", device_id=dev)
+                gather = PackedGather(W, H, world, rank, dev)
+                collective = "gather (torch.distributed nccl, fallback)"
 
     def step():
-        # render kernel(s) bracketed by HIP events the library records on this stream
-        scene.render_async(cam, prm, mine.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            if rehearse:
-                mine_h.copy_(mine)
-                gather(mine_h, frame_h, dist)
-                frame.copy_(frame_h)
-            elif collective[0] == "gather":
-                try:
-                    gather(mine, frame, dist)  # each rank's own pixels -> rank 0's frame (one gather)
-                except RuntimeError as e:  # a backend without gather: the full-frame reduce instead
-                    print(f"rank {rank}: gather failed ({e}); using reduce", file=sys.stderr, flush=True)
-                    collective[0] = "reduce"
-                    assemble_frame(mine, frame, dist, dst=0)
+        if world == 1:
+            scene.render_async(cam, prm, frame.data_ptr(), stream.cuda_stream)
+        else:
+            scene.render_packed_async(cam, prm, packed.data_ptr(), stream.cuda_stream)
+            if comm is not None:
+                comm.gather_frame_async(packed.data_ptr(), W, H, frame.data_ptr(), stream.cuda_stream)
+            elif rehearse:
+                packed_h.copy_(packed)
+                gather(packed_h, frame_h, dist)
+                if rank == 0:
+                    frame.copy_(frame_h)
             else:
-                assemble_frame(mine, frame, dist, dst=0)
+                gather(packed, frame, dist, group=nccl_group)
         if rank == 0:
             rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
                                              yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(stream.cuda_stream))
@@ -167,23 +225,25 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     render_ms, accum_ms, frames = scene.frame_timing(stream.cuda_stream)
     kern_ms = render_ms / max(1, frames)   # k_render average launch duration over the timed steps
     accum_ms = accum_ms / max(1, frames)   # k_accumulate (chunked path)
 
-    # the image really is the frame (cheap sanity: finite, non-zero)
-    if rank == 0:
+    frame_check = None
+    if rank == 0:  # the image really is the frame: finite, non-zero, and for N > 1 bitwise one device's
         f = frame.float()
         assert torch.isfinite(f).all() and f.abs().sum() > 0
-        if rehearse and world > 1:  # the assembled shards are bitwise the one-rank frame
-            full = torch.zeros_like(mine)
+        if world > 1:
+            full = torch.zeros_like(frame)
             scene.render_async(cam, yart.render_params(W, H, spp, depth), full.data_ptr(), stream.cuda_stream)
             torch.cuda.synchronize(dev)
-            assert torch.equal(full, frame), "sharded frame differs from the one-rank render"
-            print("rehearsal: sharded frame bitwise equal to the one-rank render", flush=True)
+            assert torch.equal(full, frame), "assembled frame differs from the one-device render"
+            frame_check = "assembled frame bitwise equal to the one-device render"
+            print(frame_check, file=sys.stderr, flush=True)
+            scene.frame_timing(stream.cuda_stream)
 
     roofline = None
     cpu = None
@@ -192,10 +252,13 @@ def main():
         flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
                  st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        pmc = pmc_summary()
-        traffic = pmc.get("hbm_bytes_per_launch")
+        pmc, pmc_source = pmc_snapshot()
+        traffic = pmc.get("hbm_bytes_per_launch") if world == 1 else None
         roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / F64_VALU_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "achieved_kind": "modelled: algorithmic f64 FLOPs (kernel work counters x DESIGN.md FLOP model) "
+                                     "/ HIP-event kernel time",
+                    "traffic_source": pmc_source if world == 1 else "not measured for a shard",
                     "kernel": "k_render<false,false,true>" if accum_ms > 0 else "k_render<false,false,false>",
                     "kernel_ms": round(kern_ms, 3), "accumulate_ms": round(accum_ms, 3),
                     "algorithmic_flops_per_launch": int(flops),
@@ -203,7 +266,7 @@ def main():
                                "light_tests": st.light_tests, "node_visits": st.node_visits,
                                "leaf_tris": st.leaf_tris},
                     "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None),
-                    "valu_issue_busy": valu_issue(pmc)}
+                    "valu_issue_busy": valu_issue(pmc) if world == 1 else None}
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
 
@@ -217,11 +280,12 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
             "config": {"workload": "cornell-box 800x800x256spp depth 50 (BASELINE configs[1])", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"pixel-blocks x{world}",
-                       "collective": (collective[0] + (" (gloo rehearsal)" if rehearse else " (RCCL)")) if world > 1 else None,
-                       "seed": yart.DEFAULT_SEED},
+                       "collective": collective, "frame_check": frame_check, "seed": yart.DEFAULT_SEED},
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

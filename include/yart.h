@@ -17,7 +17,10 @@
  *    (the reference panics instead: triangle.rs:113, main.rs:557, main.rs:774).
  *  - All inputs are caller-owned and copied during the call; outputs are caller-allocated.
  *  - Scene handles are immutable after yart_scene_create and may be used from several host
- *    threads at once (each call uses the stream it is given).
+ *    threads at once: the host-output calls (yart_render, yart_render_with_stats,
+ *    yart_intersect) each run on a library-owned stream of their own with their own scratch;
+ *    the *_async calls run on the caller's stream, one frame's launches enqueued atomically.
+ *    Calls on distinct devices' handles are independent.
  *  - Arithmetic is IEEE f64 throughout, as in the reference (no FMA contraction).
  */
 #ifndef YART_H
@@ -253,7 +256,9 @@ int yart_render_async(yart_scene* scene, const yart_camera* cam, const yart_rend
 int yart_frame_timing(yart_scene* scene, void* hip_stream, double* render_ms, double* accumulate_ms,
                       uint32_t* frames);
 
-/* Same, with host output and an optional progress callback (called on this thread). */
+/* Same, with host output and an optional progress callback, called on this thread while the
+ * device renders (every ~10 ms when the count moved): pixels_done is monotone, counts the covered
+ * pixels of the shard whose work has been handed out, and the last call reports all of them. */
 int yart_render(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
                 double* xyz_sum_out, yart_progress_fn progress, void* user);
 
@@ -261,6 +266,58 @@ int yart_render(yart_scene* scene, const yart_camera* cam, const yart_render_par
 int yart_render_with_stats(yart_scene* scene, const yart_camera* cam,
                            const yart_render_params* p, double* xyz_sum_out,
                            yart_render_stats* stats);
+
+/* ------------------------------------------------ multi-GPU: shards + one RCCL gather
+ * Replaces the reference's fan-out of 64 tile jobs over its thread pool and the stitching of
+ * their results into one image (main.rs:633-660, 747-760): the frame's 8x8-pixel blocks are dealt
+ * round-robin to devices (block b -> shard b % N), each device renders its blocks into a PACKED
+ * buffer and ONE gather over RCCL/xGMI brings every shard to the root, which unpacks the frame.
+ *
+ * Packed layout of shard s of N (the gather's wire format): its blocks in local order (local
+ * block j = global block s + j*N), 64 pixel slots per block (slot = (y % 8) * 8 + x % 8), 3
+ * doubles (XYZ sum) per slot; slots outside the frame or the crop grid are unspecified. */
+uint64_t yart_shard_packed_len(uint32_t width, uint32_t height, uint32_t shard_index,
+                               uint32_t shard_count); /* doubles */
+
+/* yart_render_async with the packed output (p->shard_index / shard_count select the shard). */
+int yart_render_packed_async(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
+                             double* d_packed, void* hip_stream);
+
+/* RCCL communicator over the devices of the frame, one rank per device.
+ *   one process per GPU: rank 0 calls yart_comm_unique_id, hands the 128 bytes to every rank
+ *                        (torch.distributed, MPI, a file ...), each calls yart_comm_init_rank;
+ *   one process, N GPUs: yart_comm_init_all (ncclCommInitAll), comms_out[d] for devices[d]. */
+#define YART_COMM_ID_BYTES 128
+typedef struct yart_comm yart_comm;
+int yart_comm_unique_id(uint8_t id_out[YART_COMM_ID_BYTES]);
+int yart_comm_init_rank(const uint8_t id[YART_COMM_ID_BYTES], int n_ranks, int rank, int device,
+                        yart_comm** out);
+int yart_comm_init_all(int n_devices, const int* devices, yart_comm** comms_out);
+void yart_comm_destroy(yart_comm* comm);
+
+/* Every rank's packed shard (rank r holds shard r of n_ranks, `d_packed` on its device) -> the
+ * whole W x H x 3 frame in `d_frame` on `root` (ignored elsewhere; every pixel written, 0 outside
+ * the crop grid): ONE ncclGather of equal-sized packets, then an unpack kernel on the root. Bitwise
+ * the one-device render: each pixel has exactly one writer. `d_packed` must hold
+ * yart_shard_packed_len(width, height, 0, n_ranks) doubles (the largest shard: packets are equal
+ * sized). Enqueued on `hip_stream` (the rank's
+ * device); collective — every rank must call it. Not for comms from yart_comm_init_all (use
+ * yart_render_multi, which groups the ranks' calls). */
+int yart_gather_frame_async(yart_comm* comm, const double* d_packed, uint32_t width, uint32_t height,
+                            int root, double* d_frame, void* hip_stream);
+
+/* One process driving N devices: a scene resident on each (uploaded once) and an RCCL
+ * communicator over them. yart_render_multi renders shard d on device d (all devices at once, each
+ * on its own stream), gathers the shards to devices[0] and copies the frame to host memory:
+ * bitwise yart_render on one device. Progress (if any) counts pixels over all devices and runs on
+ * the calling thread. p->shard_index / shard_count are ignored (the devices are the shards). */
+typedef struct yart_multi yart_multi;
+int yart_multi_create(int n_devices, const int* devices, const yart_scene_desc* desc, yart_multi** out);
+int yart_render_multi(yart_multi* m, const yart_camera* cam, const yart_render_params* p,
+                      double* xyz_sum_out, yart_progress_fn progress, void* user);
+/* Device time of the last yart_render_multi: render (slowest device) and gather + unpack, ms. */
+int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gather_ms);
+void yart_multi_destroy(yart_multi* m);
 
 /* main.rs:710-718: xyz * 360 / (CIE_Y_INTERGAL * spp) -> XYZ::into_rgb -> sRGB gamma ->
  * (256 * clamp(c, 0, 0.999)) as u8, alpha 255; pixels the tile grid never covers -> 0,0,0,0.

@@ -73,3 +73,12 @@ int main(void) {
             abi.SceneInfo, abi.RenderStats, abi.RenderDefaults, abi.Cli, abi.RenderOptions]
     assert [int(x) for x in got[0].split()] == [C.sizeof(t) for t in want]
     assert [int(x) for x in got[1].split()] == [abi.Object.p.offset, abi.SceneDesc.background.offset, abi.Cli.seed.offset]
+
+
+def test_shard_packed_len_is_the_packed_layout():
+    """yart_shard_packed_len (host arithmetic, no GPU) = 64 slots x 3 doubles per owned block, the
+    length yart.shard.packed_pixels enumerates."""
+    from yart.shard import packed_pixels
+    for (w, h, n) in [(800, 800, 1), (800, 800, 8), (37, 29, 3), (1920, 1080, 7)]:
+        for r in range(n):
+            assert yart.shard_packed_len(w, h, r, n) == 3 * len(packed_pixels(w, h, n, r))

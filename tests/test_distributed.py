@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 
 import oracle_lib as O
 import yart
-from yart.shard import ShardGather, assemble_frame, block_owner
+from yart.shard import PackedGather, ShardGather, assemble_frame, block_owner, packed_pixels
 
 W, H, SPP, DEPTH = 40, 24, 2, 50
 
@@ -50,11 +50,23 @@ def _worker(rank, world, port, out_path):
         g(mine2, frame2, dist)
     if rank == 0:
         np.save(out_path.replace(".npy", "_gather.npy"), frame2.numpy())
+    # bench.py's N > 1 data path: the rank's block-packed shard (libyart's wire format) and the
+    # packet gather libyart issues as one ncclGather; unused / uncovered slots hold garbage
+    pix = packed_pixels(W, H, world, rank)
+    packed = torch.full((len(pix), 3), float("nan"), dtype=torch.float64)
+    keep = pix >= 0
+    packed[torch.from_numpy(keep)] = mine.view(-1, 3)[torch.from_numpy(pix[keep])]
+    pg = PackedGather(W, H, world, rank, torch.device("cpu"))
+    frame3 = torch.zeros_like(mine)
+    for _ in range(2):
+        pg(packed, frame3, dist)
+    if rank == 0:
+        np.save(out_path.replace(".npy", "_packed.npy"), frame3.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_two_rank_gloo_frame_assembly(tmp_path, world):
     out = tmp_path / "frame.npy"
     mp.spawn(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
@@ -62,6 +74,18 @@ def test_two_rank_gloo_frame_assembly(tmp_path, world):
     full = O.OracleScene(p.desc).render(p.camera(W, H), yart.render_params(W, H, SPP, DEPTH), threads=2)
     np.testing.assert_array_equal(np.load(out), full)
     np.testing.assert_array_equal(np.load(str(out).replace(".npy", "_gather.npy")), full)
+    np.testing.assert_array_equal(np.load(str(out).replace(".npy", "_packed.npy")), full)
+
+
+def test_packed_pixels_partition_the_covered_frame():
+    for (w, h, n) in [(40, 24, 2), (37, 29, 3), (400, 225, 8), (1920, 1080, 8)]:
+        seen = np.concatenate([packed_pixels(w, h, n, r) for r in range(n)])
+        seen = seen[seen >= 0]
+        assert len(seen) == len(np.unique(seen))
+        cov = O.coverage(w, h).reshape(-1)
+        assert set(seen.tolist()) == set(np.flatnonzero(cov).tolist())
+        # shard 0 is the largest packet (ncclGather's equal-size packets)
+        assert all(len(packed_pixels(w, h, n, r)) <= len(packed_pixels(w, h, n, 0)) for r in range(n))
 
 
 def test_block_owner_matches_shard_renders():

@@ -1,0 +1,68 @@
+"""Parity at the BASELINE.json configurations themselves, on the production work plan.
+
+The GPU renders each config's FULL frame exactly as bench.py / tools/bench_configs.py do (one
+yart_render call, samples_per_unit = 0: the library's own chunk/pass plan, so C2 runs the
+8-10-spp units of its persistent-wave plan and C5 the multi-pass scratch path). The oracle
+(oracle/, the CPU restatement of main.rs:628-708) then renders either the same full frame (C1, C2:
+cheap enough) or only a fixed, spread subset of 8x8 blocks (b % stride == 0, through the same
+shard rule), and the two must be BITWISE equal on every pixel the oracle rendered.
+
+Sizes: C1 two-spheres 400x225x16 d8, C2 cornell-box 800x800x256 d50, C3 random-scene
+1200x800x500, C4 bunny (sycee stand-in) 800x800x512, C5 david 1920x1080x1024 d50.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import yart
+
+pytestmark = pytest.mark.gpu
+
+# oracle threads: the GPU box's CPU share is 16 (os.cpu_count() there reports the whole machine)
+THREADS = min(16, os.cpu_count() or 1)
+
+# config, scene, W, H, spp, depth, oracle block stride (1 = the whole frame)
+CONFIGS = [
+    ("C1", "two-spheres", 400, 225, 16, 8, 1),
+    ("C2", "cornell-box", 800, 800, 256, 50, 1),
+    ("C3", "random-scene", 1200, 800, 500, 50, 97),
+    ("C4", "bunny", 800, 800, 512, 50, 61),
+    ("C5", "david", 1920, 1080, 1024, 50, 997),
+]
+
+
+def block_mask(w, h, stride):
+    bx = (w + 7) // 8
+    ys, xs = np.mgrid[0:h, 0:w]
+    return (((ys // 8) * bx + (xs // 8)) % stride) == 0
+
+
+@pytest.mark.parametrize("cfg,scene,W,H,spp,depth,stride", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_config_full_frame_bitwise(cfg, scene, W, H, spp, depth, stride):
+    p = yart.Preset(scene)
+    cam = p.camera(W, H)
+    s = yart.DeviceScene(p)
+    gpu = s.render(cam, yart.render_params(W, H, spp, depth))  # production plan (samples_per_unit = 0)
+    assert np.isfinite(gpu).all()
+    cov = O.coverage(W, H)
+    assert (gpu[~cov] == 0).all()
+    oracle = O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, depth, shard_index=0, shard_count=stride),
+                                          threads=THREADS)
+    m = block_mask(W, H, stride) & cov
+    assert m.sum() >= 64 * 8, "the subset must hold several blocks"
+    bad = np.argwhere((gpu != oracle).any(axis=-1) & m)
+    assert len(bad) == 0, f"{cfg}: {len(bad)} of {m.sum()} checked pixels differ, e.g. (y, x) {bad[:4].tolist()}"
+    # the oracle rendered nothing outside its blocks; the GPU rendered everything covered
+    assert (oracle[~m] == 0).all()
+    assert (gpu[cov].sum(axis=-1) != 0).mean() > 0.5
+
+
+def test_c5_runs_the_multi_pass_scratch_path():
+    """C5 on one device does not fit the 4 GiB per-sample scratch in one pass (49.8 MB per sample);
+    the plan must split it, which is what test_config_full_frame_bitwise[C5] then exercises."""
+    W, H, spp = 1920, 1080, 1024
+    per_sample = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 3 * 8
+    assert per_sample * spp > 4 << 30
+    assert (4 << 30) // per_sample < spp

@@ -28,6 +28,11 @@ def per_launch(pass_dir, kernel):
     return {k: sum(v.values()) / len(v) for k, v in vals.items()}, rows
 
 
+def kernels_sha256():
+    import hashlib
+    return hashlib.sha256((ROOT / "yet-another-raytracer_amd" / "csrc" / "kernels.hip").read_bytes()).hexdigest()
+
+
 def main():
     tag = sys.argv[1]
     kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<false, false, true>"
@@ -56,6 +61,9 @@ def main():
     if fetch is not None and write is not None:
         summary["hbm_bytes_per_launch"] = int(fetch * 1024 * 2 + write * 1024)
         summary["hbm_bytes_note"] = "FETCH_SIZE x2 (gfx950 reports half of wide reads) + WRITE_SIZE, KiB -> B"
+    # which kernel source the counters belong to: bench.py reports the traffic only while
+    # csrc/kernels.hip still hashes to this value
+    summary["kernels_sha256"] = kernels_sha256()
     (PROF / f"{tag}_pmc.json").write_text(json.dumps(summary, indent=1) + "\n")
     if "cornell" in tag or tag.endswith("_render"):
         (PROF / "pmc_render_cornell.json").write_text(json.dumps(summary, indent=1) + "\n")

@@ -1,6 +1,7 @@
 // capi.cpp — the C ABI of include/yart.h: scene upload to HBM, launches, host conveniences.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -9,33 +10,33 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/yart.h"
 #include "../host/camera_impl.h"
 #include "bvh_build.h"
 #include "kernels.h"
+#include "scene_impl.h"
 #include "world_bvh.h"
 
 using namespace yart_dev;
+using namespace yart_impl;
 
-namespace {
-
-// Object lists at least this long get a world BVH (the random scene has ~485 spheres; the
-// cornell box's 8 entries are walked linearly).
-constexpr uint32_t kWorldBvhMinObjects = 16;
-
+namespace yart_impl {
 thread_local std::string g_err;
 int fail(int code, const std::string& m) { g_err = m; return code; }
 int ok() { g_err.clear(); return YART_OK; }
 int hip_fail(hipError_t e, const char* what) {
   return fail(YART_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
-#define HIP_TRY(expr, what)                      \
-  do {                                           \
-    hipError_t e_ = (expr);                      \
-    if (e_ != hipSuccess) return hip_fail(e_, what); \
-  } while (0)
+}  // namespace yart_impl
+
+namespace {
+
+// Object lists at least this long get a world BVH (the random scene has ~485 spheres; the
+// cornell box's 8 entries are walked linearly).
+constexpr uint32_t kWorldBvhMinObjects = 16;
 
 // Smits basis spectra (color.rs:1711-1982): white, cyan, magenta, yellow, red, green, blue.
 const double kSmits[7][36] = {
@@ -62,14 +63,6 @@ double spectrum_bin(const double rgb[3], int i) {
   }
   return s;
 }
-
-class DeviceGuard {  // keep the caller's current device (torch tracks its own)
- public:
-  explicit DeviceGuard(int dev) { (void)hipGetDevice(&old_); if (old_ != dev) (void)hipSetDevice(dev); dev_ = dev; }
-  ~DeviceGuard() { if (old_ != dev_) (void)hipSetDevice(old_); }
- private:
-  int old_ = 0, dev_ = 0;
-};
 
 template <class T>
 hipError_t upload(std::vector<void*>& owned, const T* src, size_t n, const T** dst, uint64_t& bytes) {
@@ -122,28 +115,16 @@ DevObject to_dev(const yart_object& o) {
 
 }  // namespace
 
-struct yart_scene {
-  int device = 0;
-  int cu_count = 256;
-  DevScene dev{};
-  std::vector<void*> owned;
-  yart_scene_info info{};
-  // Per-stream scratch for the chunked render path (grown on demand, reused across frames).
-  std::mutex scratch_mu;
-  std::map<hipStream_t, std::pair<double*, size_t>> scratch;
-  // kernel-boundary events of the frames launched per stream and not yet read
-  std::map<hipStream_t, std::vector<std::vector<hipEvent_t>>> frames;
-  std::vector<hipEvent_t> event_pool;
-  ~yart_scene() {
-    DeviceGuard g(device);
-    for (void* p : owned) (void)hipFree(p);
-    for (auto& kv : scratch) (void)hipFree(kv.second.first);
-    for (auto& kv : frames)
-      for (auto& f : kv.second)
-        for (hipEvent_t e : f) (void)hipEventDestroy(e);
-    for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
-  }
-};
+yart_scene::~yart_scene() {
+  DeviceGuard g(device);
+  for (void* p : owned) (void)hipFree(p);
+  for (auto& kv : streams) (void)hipFree(kv.second->scratch);
+  for (hipStream_t st : owned_streams) (void)hipStreamDestroy(st);
+  for (auto& kv : frames)
+    for (auto& f : kv.second)
+      for (hipEvent_t e : f) (void)hipEventDestroy(e);
+  for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
+}
 
 extern "C" {
 
@@ -314,26 +295,49 @@ int yart_scene_get_info(const yart_scene* s, yart_scene_info* out) {
   return ok();
 }
 
-static int make_args(const yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* out,
-                     RenderArgs& a) {
+}  // extern "C"
+
+namespace yart_impl {
+
+int make_args(const yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* out, RenderArgs& a) {
   if (!s || !cam || !p) return fail(YART_ERR_INVALID, "null argument");
   if (p->width == 0 || p->height == 0) return fail(YART_ERR_INVALID, "width and height must be > 0");
   if ((uint64_t)p->width * p->height > 0xFFFFFFFFull) return fail(YART_ERR_INVALID, "image too large (pixel index is 32-bit)");
   const uint32_t sc = p->shard_count ? p->shard_count : 1;
   if (p->shard_index >= sc) return fail(YART_ERR_INVALID, "shard_index >= shard_count");
+  a = RenderArgs{};
   a.cam = *cam;
   a.width = p->width; a.height = p->height; a.spp = p->spp; a.max_depth = p->max_depth; a.seed = p->seed;
   a.shard_index = p->shard_index; a.shard_count = sc;
   a.blocks_x = (p->width + 7) / 8;
-  const uint32_t total = a.blocks_x * ((p->height + 7) / 8);
-  a.n_blocks = total > p->shard_index ? (total - p->shard_index + sc - 1) / sc : 0;
+  a.n_blocks = shard_blocks(a.blocks_x * ((p->height + 7) / 8), p->shard_index, sc);
   a.s_begin = 0; a.s_count = p->spp; a.chunk = p->spp ? p->spp : 1; a.n_chunks = 1;
   a.out = out;
-  a.scratch = nullptr;
-  a.stats = nullptr;
-  a.queue = nullptr; a.n_units = 0; a.waves = 0;
   return YART_OK;
 }
+
+uint64_t shard_pixels(uint32_t w, uint32_t h, uint32_t shard_index, uint32_t shard_count) {
+  // covered columns / rows per 8-pixel block column / row (main.rs:636-647)
+  const uint32_t bx = (w + 7) / 8, by = (h + 7) / 8;
+  auto per_block = [](uint32_t n, uint32_t nb) {
+    std::vector<uint32_t> c(nb, 0);
+    const uint32_t cw = n / 8;
+    for (uint32_t col = 0; col < 8; ++col) {
+      const uint32_t x0 = (uint32_t)(((uint64_t)n * col) / 8);
+      for (uint32_t x = x0; x < x0 + cw && x < n; ++x) c[x / 8]++;
+    }
+    return c;
+  };
+  const std::vector<uint32_t> cx = per_block(w, bx), cy = per_block(h, by);
+  const uint32_t sc = shard_count ? shard_count : 1;
+  uint64_t n = 0;
+  for (uint64_t b = shard_index; b < (uint64_t)bx * by; b += sc) n += (uint64_t)cx[b % bx] * cy[b / bx];
+  return n;
+}
+
+}  // namespace yart_impl
+
+namespace {
 
 // Work decomposition. A unit is one wave rendering one 8x8 block for `chunk` consecutive samples.
 // With chunk = spp (one unit per block) the kernel keeps the per-pixel sums in registers (fused).
@@ -341,7 +345,7 @@ static int make_args(const yart_scene* s, const yart_camera* cam, const yart_ren
 // frames) the samples are split into chunks; each sample's value then goes to HBM and
 // k_accumulate adds them per pixel in sample order, so the sums do not depend on the split.
 struct Plan { uint32_t chunk, pass_spp; };
-static Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
+Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
   const uint32_t spp = a.spp;
   if (spp == 0 || a.n_blocks == 0) return {spp ? spp : 1, spp};
   uint32_t chunk;
@@ -367,61 +371,87 @@ static Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
   return {chunk, (uint32_t)pass};
 }
 
-static int get_scratch(yart_scene* s, hipStream_t stream, size_t bytes, double** out) {
-  std::lock_guard<std::mutex> lk(s->scratch_mu);
-  auto& e = s->scratch[stream];
-  if (e.second < bytes) {
-    if (e.first) HIP_TRY(hipFree(e.first), "hipFree scratch");
-    e.first = nullptr; e.second = 0;
-    HIP_TRY(hipMalloc(&e.first, bytes), "hipMalloc scratch");
-    e.second = bytes;
+StreamState* stream_state(yart_scene* s, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto& e = s->streams[stream];
+  if (!e) e = std::make_unique<StreamState>();
+  return e.get();
+}
+
+// Scratch of a stream, grown on demand. Called with st->frame_mu held: no other frame of this
+// library is being enqueued on the stream; earlier frames may still run on it, so the old buffer
+// is released only after the stream drained.
+int stream_scratch(StreamState* st, hipStream_t stream, size_t bytes, double** out) {
+  if (st->bytes < bytes) {
+    if (st->scratch) {
+      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its scratch");
+      HIP_TRY(hipFree(st->scratch), "hipFree scratch");
+    }
+    st->scratch = nullptr; st->bytes = 0;
+    HIP_TRY(hipMalloc(&st->scratch, bytes), "hipMalloc scratch");
+    st->bytes = bytes;
   }
-  *out = e.first;
+  *out = st->scratch;
   return YART_OK;
 }
 
-// HIP events around every kernel of each frame launched on a stream, kept until
-// yart_frame_timing reads (and recycles) them.
-static int timing_events(yart_scene* s, hipStream_t stream, size_t n, std::vector<hipEvent_t>** out) {
-  std::lock_guard<std::mutex> lk(s->scratch_mu);
-  auto& frames = s->frames[stream];
-  if (frames.size() >= 4096) {  // never read: recycle the oldest frame's events
-    for (hipEvent_t e : frames.front()) s->event_pool.push_back(e);
-    frames.erase(frames.begin());
-  }
-  std::vector<hipEvent_t> f;
+// n timing events for one frame (copied out: the caller owns them until push_frame hands them over).
+int take_events(yart_scene* s, size_t n, std::vector<hipEvent_t>& f) {
+  f.clear();
+  std::lock_guard<std::mutex> lk(s->mu);
   while (f.size() < n) {
     if (!s->event_pool.empty()) {
       f.push_back(s->event_pool.back());
       s->event_pool.pop_back();
     } else {
       hipEvent_t e;
-      HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+      hipError_t err = hipEventCreate(&e);
+      if (err != hipSuccess) {
+        for (hipEvent_t x : f) s->event_pool.push_back(x);
+        f.clear();
+        return hip_fail(err, "hipEventCreate");
+      }
       f.push_back(e);
     }
   }
-  frames.push_back(std::move(f));
-  *out = &frames.back();
   return YART_OK;
 }
+void push_frame(yart_scene* s, hipStream_t stream, std::vector<hipEvent_t>&& f) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto& frames = s->frames[stream];
+  if (frames.size() >= 4096) {  // never read: recycle the oldest frame's events
+    for (hipEvent_t e : frames.front()) s->event_pool.push_back(e);
+    frames.erase(frames.begin());
+  }
+  frames.push_back(std::move(f));
+}
 
-static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream) {
+}  // namespace
+
+namespace yart_impl {
+
+int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream, Progress* prog) {
   const Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
-  std::vector<hipEvent_t>* ev = nullptr;
+  StreamState* st = stream_state(s, stream);
+  std::lock_guard<std::mutex> frame_lock(st->frame_mu);
+  std::vector<hipEvent_t> ev;
+  if (prog) a.progress = prog->device;
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
-    if (int rc = timing_events(s, stream, 2, &ev)) return rc;
-    HIP_TRY(hipEventRecord((*ev)[0], stream), "hipEventRecord");
+    if (prog) prog->total_units = a.n_blocks;
+    if (int rc = take_events(s, 2, ev)) return rc;
+    HIP_TRY(hipEventRecord(ev[0], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, a, stats, stream), "launch k_render");
-    HIP_TRY(hipEventRecord((*ev)[1], stream), "hipEventRecord");
+    HIP_TRY(hipEventRecord(ev[1], stream), "hipEventRecord");
+    push_frame(s, stream, std::move(ev));
     return YART_OK;
   }
   double* scratch = nullptr;
   const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
-  if (int rc = get_scratch(s, stream, scratch_bytes + 256, &scratch)) return rc;  // + the unit counter
+  if (int rc = stream_scratch(st, stream, scratch_bytes + 256, &scratch)) return rc;  // + the unit counter
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + scratch_bytes);
   const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
-  if (int rc = timing_events(s, stream, 3 * (size_t)passes, &ev)) return rc;
-  uint32_t k = 0;
+  if (int rc = take_events(s, 3 * (size_t)passes, ev)) return rc;
+  uint32_t k = 0, base = 0;
   for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp, ++k) {
     RenderArgs b = a;
     b.s_begin = s0;
@@ -432,43 +462,126 @@ static int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool st
     b.queue = queue;
     b.n_units = b.n_blocks * b.n_chunks;
     b.waves = (uint32_t)s->cu_count * 16;  // 4 waves per SIMD resident
+    b.progress_base = base;
+    base += b.n_units;
     HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream), "zero the unit counter");
-    HIP_TRY(hipEventRecord((*ev)[3 * k], stream), "hipEventRecord");
+    HIP_TRY(hipEventRecord(ev[3 * k], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
-    HIP_TRY(hipEventRecord((*ev)[3 * k + 1], stream), "hipEventRecord");
+    HIP_TRY(hipEventRecord(ev[3 * k + 1], stream), "hipEventRecord");
     HIP_TRY(launch_accumulate(b, s0 == 0, stream), "launch k_accumulate");
-    HIP_TRY(hipEventRecord((*ev)[3 * k + 2], stream), "hipEventRecord");
+    HIP_TRY(hipEventRecord(ev[3 * k + 2], stream), "hipEventRecord");
   }
+  if (prog) prog->total_units = base;
+  push_frame(s, stream, std::move(ev));
   return YART_OK;
 }
+
+int acquire_stream(yart_scene* s, hipStream_t* out) {
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (!s->idle_streams.empty()) {
+      *out = s->idle_streams.back();
+      s->idle_streams.pop_back();
+      return YART_OK;
+    }
+  }
+  DeviceGuard g(s->device);
+  hipStream_t st;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->owned_streams.push_back(st);
+  *out = st;
+  return YART_OK;
+}
+void release_stream(yart_scene* s, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->idle_streams.push_back(st);
+}
+
+int alloc_progress(Progress& p) {
+  void* h = nullptr;
+  HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc progress word");
+  p.host = static_cast<uint32_t*>(h);
+  __atomic_store_n(p.host, 0u, __ATOMIC_RELAXED);
+  void* d = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) { (void)hipHostFree(h); p.host = nullptr; return hip_fail(e, "hipHostGetDevicePointer"); }
+  p.device = static_cast<uint32_t*>(d);
+  return YART_OK;
+}
+void free_progress(Progress& p) {
+  if (p.host) (void)hipHostFree(p.host);
+  p.host = p.device = nullptr;
+}
+
+int wait_with_progress(const std::vector<hipEvent_t>& done, const std::vector<int>& devices,
+                       const std::vector<Progress*>& prog, uint64_t total_pixels, yart_progress_fn fn, void* user) {
+  uint64_t reported = 0;
+  for (size_t i = 0; i < done.size(); ++i) {
+    DeviceGuard g(devices[i]);
+    for (;;) {
+      const hipError_t q = hipEventQuery(done[i]);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return hip_fail(q, "render");
+      if (fn) {
+        // pixels of the frame whose units have been handed out, over all devices
+        uint64_t units = 0, total = 0, px = 0;
+        for (Progress* p : prog) {
+          const uint32_t u = __atomic_load_n(p->host, __ATOMIC_RELAXED);
+          units = u < p->total_units ? u : p->total_units;
+          total = p->total_units ? p->total_units : 1;
+          px += p->pixels * units / total;
+        }
+        if (px > reported && px < total_pixels) {
+          reported = px;
+          fn(px, user);
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(fn ? 10 : 1));
+    }
+  }
+  if (fn && reported < total_pixels) fn(total_pixels, user);
+  return YART_OK;
+}
+
+}  // namespace yart_impl
+
+extern "C" {
 
 int yart_frame_timing(yart_scene* s, void* stream, double* render_ms, double* accumulate_ms, uint32_t* frames) {
   if (!s || !render_ms || !accumulate_ms || !frames) return fail(YART_ERR_INVALID, "null argument");
   DeviceGuard g(s->device);
-  std::lock_guard<std::mutex> lk(s->scratch_mu);
-  auto it = s->frames.find((hipStream_t)stream);
+  std::vector<std::vector<hipEvent_t>> mine;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    auto it = s->frames.find((hipStream_t)stream);
+    if (it != s->frames.end()) mine.swap(it->second);
+  }
   double r = 0.0, acc = 0.0;
   uint32_t n_frames = 0;
-  if (it != s->frames.end()) {
-    for (const auto& v : it->second) {
-      float ms = 0.0f;
-      if (v.size() == 2) {
-        HIP_TRY(hipEventElapsedTime(&ms, v[0], v[1]), "hipEventElapsedTime");
+  int rc = YART_OK;
+  for (const auto& v : mine) {
+    float ms = 0.0f;
+    hipError_t e = hipSuccess;
+    if (v.size() == 2) {
+      if ((e = hipEventElapsedTime(&ms, v[0], v[1])) == hipSuccess) r += ms;
+    } else {
+      for (size_t k = 0; k + 2 < v.size() && e == hipSuccess; k += 3) {
+        if ((e = hipEventElapsedTime(&ms, v[k], v[k + 1])) != hipSuccess) break;
         r += ms;
-      } else {
-        for (size_t k = 0; k + 2 < v.size(); k += 3) {
-          HIP_TRY(hipEventElapsedTime(&ms, v[k], v[k + 1]), "hipEventElapsedTime");
-          r += ms;
-          HIP_TRY(hipEventElapsedTime(&ms, v[k + 1], v[k + 2]), "hipEventElapsedTime");
-          acc += ms;
-        }
+        if ((e = hipEventElapsedTime(&ms, v[k + 1], v[k + 2])) != hipSuccess) break;
+        acc += ms;
       }
-      ++n_frames;
     }
-    for (auto& v : it->second)
-      for (hipEvent_t e : v) s->event_pool.push_back(e);
-    it->second.clear();
+    if (e != hipSuccess && rc == YART_OK) rc = hip_fail(e, "hipEventElapsedTime");
+    ++n_frames;
   }
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    for (auto& v : mine)
+      for (hipEvent_t e : v) s->event_pool.push_back(e);
+  }
+  if (rc != YART_OK) return rc;
   *render_ms = r;
   *accumulate_ms = acc;
   *frames = n_frames;
@@ -481,53 +594,96 @@ int yart_render_async(yart_scene* s, const yart_camera* cam, const yart_render_p
   if (int rc = make_args(s, cam, p, d_xyz_sum, a)) return rc;
   if (!d_xyz_sum) return fail(YART_ERR_INVALID, "null output");
   DeviceGuard g(s->device);
-  if (int rc = launch_frame(s, a, p->samples_per_unit, false, (hipStream_t)stream)) return rc;
+  if (int rc = launch_frame(s, a, p->samples_per_unit, false, (hipStream_t)stream, nullptr)) return rc;
   return ok();
 }
 
-static int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* host_out,
-                       yart_render_stats* stats) {
+int yart_render_packed_async(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* d_packed,
+                             void* stream) {
+  RenderArgs a;
+  if (int rc = make_args(s, cam, p, d_packed, a)) return rc;
+  if (!d_packed) return fail(YART_ERR_INVALID, "null output");
+  a.packed = 1;
+  DeviceGuard g(s->device);
+  if (int rc = launch_frame(s, a, p->samples_per_unit, false, (hipStream_t)stream, nullptr)) return rc;
+  return ok();
+}
+
+uint64_t yart_shard_packed_len(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count) {
+  const uint32_t sc = shard_count ? shard_count : 1;
+  return (uint64_t)shard_blocks(((width + 7) / 8) * ((height + 7) / 8), shard_index, sc) * 64 * 3;
+}
+
+}  // extern "C"
+
+namespace {
+
+// yart_render / yart_render_with_stats: a library-owned stream per call (so concurrent calls on
+// one handle, from several host threads, never share a stream, a scratch buffer or a unit
+// counter), device output on it, one copy back, progress polled on the calling thread.
+int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* host_out,
+                yart_render_stats* stats, yart_progress_fn progress, void* user) {
   RenderArgs a;
   if (int rc = make_args(s, cam, p, nullptr, a)) return rc;
   if (!host_out) return fail(YART_ERR_INVALID, "null output");
   DeviceGuard g(s->device);
+  hipStream_t stream;
+  if (int rc = acquire_stream(s, &stream)) return rc;
+  struct Release {
+    yart_scene* s; hipStream_t st;
+    ~Release() { (void)hipStreamSynchronize(st); release_stream(s, st); }
+  } release{s, stream};
   const size_t bytes = sizeof(double) * 3 * (size_t)p->width * p->height;
   double* d_out = nullptr;
   unsigned long long* d_stats = nullptr;
   HIP_TRY(hipMalloc(&d_out, bytes), "hipMalloc output");
   std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
-  HIP_TRY(hipMemset(d_out, 0, bytes), "hipMemset");
+  HIP_TRY(hipMemsetAsync(d_out, 0, bytes, stream), "hipMemset");
   if (stats) {
     HIP_TRY(hipMalloc(&d_stats, 8 * sizeof(unsigned long long)), "hipMalloc stats");
-    HIP_TRY(hipMemset(d_stats, 0, 8 * sizeof(unsigned long long)), "hipMemset");
+    HIP_TRY(hipMemsetAsync(d_stats, 0, 8 * sizeof(unsigned long long), stream), "hipMemset");
   }
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
   a.stats = d_stats;
-  if (int rc = launch_frame(s, a, p->samples_per_unit, stats != nullptr, nullptr)) return rc;
-  HIP_TRY(hipDeviceSynchronize(), "k_render");
-  HIP_TRY(hipMemcpy(host_out, d_out, bytes, hipMemcpyDeviceToHost), "copy output");
+  Progress pr;
+  if (progress) {
+    if (int rc = alloc_progress(pr)) return rc;
+    pr.pixels = shard_pixels(p->width, p->height, a.shard_index, a.shard_count);
+  }
+  struct FreeProgress { Progress& p; ~FreeProgress() { free_progress(p); } } free_pr{pr};
+  if (int rc = launch_frame(s, a, p->samples_per_unit, stats != nullptr, stream, progress ? &pr : nullptr)) return rc;
+  hipEvent_t done;
+  HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate");
+  std::unique_ptr<std::remove_pointer<hipEvent_t>::type, decltype(&hipEventDestroy)> hold3(done, &hipEventDestroy);
+  HIP_TRY(hipEventRecord(done, stream), "hipEventRecord");
+  if (int rc = wait_with_progress({done}, {s->device}, {&pr}, pr.pixels, progress, user)) return rc;
+  HIP_TRY(hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, stream), "copy output");
   if (stats) {
     unsigned long long v[8];
-    HIP_TRY(hipMemcpy(v, d_stats, sizeof v, hipMemcpyDeviceToHost), "copy stats");
+    HIP_TRY(hipMemcpyAsync(v, d_stats, sizeof v, hipMemcpyDeviceToHost, stream), "copy stats");
+    HIP_TRY(hipStreamSynchronize(stream), "copy stats");
     std::memset(stats, 0, sizeof *stats);
     stats->samples = v[0]; stats->segments = v[1]; stats->prim_tests = v[2]; stats->node_visits = v[3];
     stats->leaf_visits = v[4]; stats->leaf_tris = v[5]; stats->light_tests = v[6];
   }
+  HIP_TRY(hipStreamSynchronize(stream), "copy output");
   return ok();
 }
 
+}  // namespace
+
+extern "C" {
+
 int yart_render(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* xyz_sum_out,
                 yart_progress_fn progress, void* user) {
-  int rc = render_host(s, cam, p, xyz_sum_out, nullptr);
-  if (rc == YART_OK && progress) progress((uint64_t)p->width * p->height, user);
-  return rc;
+  return render_host(s, cam, p, xyz_sum_out, nullptr, progress, user);
 }
 
 int yart_render_with_stats(yart_scene* s, const yart_camera* cam, const yart_render_params* p, double* xyz_sum_out,
                            yart_render_stats* stats) {
   if (!stats) return fail(YART_ERR_INVALID, "null stats");
-  return render_host(s, cam, p, xyz_sum_out, stats);
+  return render_host(s, cam, p, xyz_sum_out, stats, nullptr, nullptr);
 }
 
 int yart_finalize_rgba8_async(int device, const double* d_xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* d_rgba,
@@ -550,7 +706,7 @@ int yart_finalize_rgba8(int device, const double* xyz, uint32_t w, uint32_t h, u
   std::unique_ptr<uint8_t, decltype(&hipFree)> h2(dr, &hipFree);
   HIP_TRY(hipMemcpy(dx, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice), "copy in");
   HIP_TRY(launch_finalize(dx, w, h, spp, dr, nullptr), "launch k_finalize");
-  HIP_TRY(hipDeviceSynchronize(), "k_finalize");
+  HIP_TRY(hipStreamSynchronize(nullptr), "k_finalize");
   HIP_TRY(hipMemcpy(rgba, dr, 4 * n, hipMemcpyDeviceToHost), "copy out");
   return ok();
 }
@@ -559,6 +715,12 @@ int yart_intersect(yart_scene* s, const double* rays, uint32_t n, double* hits, 
   if (!s || (n && (!rays || !hits || !obj))) return fail(YART_ERR_INVALID, "null argument");
   if (n == 0) return ok();
   DeviceGuard g(s->device);
+  hipStream_t st;
+  if (int rc = acquire_stream(s, &st)) return rc;
+  struct Release {
+    yart_scene* s; hipStream_t st;
+    ~Release() { (void)hipStreamSynchronize(st); release_stream(s, st); }
+  } release{s, st};
   double *dr = nullptr, *dh = nullptr;
   int32_t* dobj = nullptr;
   HIP_TRY(hipMalloc(&dr, sizeof(double) * 8 * (size_t)n), "hipMalloc");
@@ -567,11 +729,11 @@ int yart_intersect(yart_scene* s, const double* rays, uint32_t n, double* hits, 
   std::unique_ptr<double, decltype(&hipFree)> h2(dh, &hipFree);
   HIP_TRY(hipMalloc(&dobj, sizeof(int32_t) * (size_t)n), "hipMalloc");
   std::unique_ptr<int32_t, decltype(&hipFree)> h3(dobj, &hipFree);
-  HIP_TRY(hipMemcpy(dr, rays, sizeof(double) * 8 * (size_t)n, hipMemcpyHostToDevice), "copy rays");
-  HIP_TRY(launch_intersect(s->dev, dr, n, dh, dobj, nullptr), "launch k_intersect");
-  HIP_TRY(hipDeviceSynchronize(), "k_intersect");
-  HIP_TRY(hipMemcpy(hits, dh, sizeof(double) * 8 * (size_t)n, hipMemcpyDeviceToHost), "copy hits");
-  HIP_TRY(hipMemcpy(obj, dobj, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost), "copy obj");
+  HIP_TRY(hipMemcpyAsync(dr, rays, sizeof(double) * 8 * (size_t)n, hipMemcpyHostToDevice, st), "copy rays");
+  HIP_TRY(launch_intersect(s->dev, dr, n, dh, dobj, st), "launch k_intersect");
+  HIP_TRY(hipMemcpyAsync(hits, dh, sizeof(double) * 8 * (size_t)n, hipMemcpyDeviceToHost, st), "copy hits");
+  HIP_TRY(hipMemcpyAsync(obj, dobj, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, st), "copy obj");
+  HIP_TRY(hipStreamSynchronize(st), "k_intersect");
   return ok();
 }
 
@@ -582,7 +744,7 @@ int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, u
   HIP_TRY(hipMalloc(&d, sizeof(double) * n), "hipMalloc");
   std::unique_ptr<double, decltype(&hipFree)> h(d, &hipFree);
   HIP_TRY(launch_probe_rng(seed, pixel, sample, n, d, nullptr), "launch k_probe_rng");
-  HIP_TRY(hipDeviceSynchronize(), "k_probe_rng");
+  HIP_TRY(hipStreamSynchronize(nullptr), "k_probe_rng");
   HIP_TRY(hipMemcpy(out, d, sizeof(double) * n, hipMemcpyDeviceToHost), "copy");
   return ok();
 }
@@ -600,7 +762,7 @@ int yart_probe_math(int device, int op, const double* a, const double* b, uint32
   HIP_TRY(hipMemcpy(da, a, sizeof(double) * n, hipMemcpyHostToDevice), "copy a");
   HIP_TRY(hipMemcpy(db, b ? b : a, sizeof(double) * n, hipMemcpyHostToDevice), "copy b");
   HIP_TRY(launch_probe_math(op, da, db, n, dout, nullptr), "launch k_probe_math");
-  HIP_TRY(hipDeviceSynchronize(), "k_probe_math");
+  HIP_TRY(hipStreamSynchronize(nullptr), "k_probe_math");
   HIP_TRY(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost), "copy out");
   return ok();
 }

@@ -1593,7 +1593,12 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         if (next_job >= n_jobs) {  // claim the next unit
           const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
           uint32_t v = 0;
-          if (lane == first) v = atomicAdd(A.queue, 1u);
+          if (lane == first) {
+            v = atomicAdd(A.queue, 1u);
+            if (A.progress)  // yart_render's progress: the units handed out so far (host-mapped word)
+              __hip_atomic_store(A.progress, A.progress_base + (v < A.n_units ? v + 1u : A.n_units), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          }
           const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)first);
           if (u >= A.n_units) { drained = true; break; }
           local_blk = u % A.n_blocks; chunk_id = u / A.n_blocks;
@@ -1834,9 +1839,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     }
   }
   if (!DYN && active) {
-    double* o = A.out + 3 * (size_t)pixel;
+    double* o = A.out + 3 * (A.packed ? (size_t)local_blk * 64 + lane : (size_t)pixel);
     o[0] = acc0; o[1] = acc1; o[2] = acc2;
   }
+  if (!DYN && A.progress && lane == 0)
+    __hip_atomic_store(A.progress, A.progress_base + (blockIdx.x + 1u) * 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (STATS) {
     for (int i = 0; i < 8; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
@@ -1852,7 +1859,7 @@ __global__ __launch_bounds__(256) void k_accumulate(RenderArgs A, int first_pass
   const uint32_t b = A.shard_index + local_blk * A.shard_count;
   const uint32_t x = (b % A.blocks_x) * 8 + (lane & 7u), y = (b / A.blocks_x) * 8 + (lane >> 3);
   if (!(x < A.width && y < A.height && covered(x, A.width) && covered(y, A.height))) return;
-  double* o = A.out + 3 * ((size_t)y * A.width + x);
+  double* o = A.out + 3 * (A.packed ? (size_t)i : (size_t)y * A.width + x);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
   if (!first_pass) { a0 = o[0]; a1 = o[1]; a2 = o[2]; }
   const double* q = A.scratch + 3 * ((size_t)local_blk * A.s_count * 64 + lane);
@@ -1862,6 +1869,25 @@ __global__ __launch_bounds__(256) void k_accumulate(RenderArgs A, int first_pass
     q += 64 * 3;
   }
   o[0] = a0; o[1] = a1; o[2] = a2;
+}
+
+// Root side of the frame gather (yart_gather_frame_async): every shard's block-packed pixels,
+// shard r at recv + r * stride, back into the W x H frame; pixel (x, y) lives in global block
+// b = (y / 8) * ceil(W / 8) + x / 8, i.e. shard b % N, local block b / N, slot (y % 8) * 8 + x % 8.
+// Writes every pixel (0 outside the crop grid), so the frame needs no clearing.
+__global__ __launch_bounds__(256) void k_unpack_shards(const double* __restrict__ recv, uint32_t shards, size_t stride,
+                                                       uint32_t w, uint32_t h, double* __restrict__ frame) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w * h) return;
+  const uint32_t x = i % w, y = i / w;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+  if (covered(x, w) && covered(y, h)) {
+    const uint32_t b = (y >> 3) * ((w + 7u) >> 3) + (x >> 3);
+    const double* q = recv + (size_t)(b % shards) * stride + 3 * ((size_t)(b / shards) * 64 + (y & 7u) * 8 + (x & 7u));
+    v0 = q[0]; v1 = q[1]; v2 = q[2];
+  }
+  double* o = frame + 3 * (size_t)i;
+  o[0] = v0; o[1] = v1; o[2] = v2;
 }
 
 // ------------------------------------------------------------------- batched closest hit
@@ -1998,6 +2024,13 @@ hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hip
     if (s.has_ext) YART_LAUNCH(false, false, true); else YART_LAUNCH(false, false, false);
   }
 #undef YART_LAUNCH
+  return hipGetLastError();
+}
+hipError_t launch_unpack_shards(const double* recv, uint32_t shards, size_t stride, uint32_t w, uint32_t h, double* frame,
+                                hipStream_t stream) {
+  const uint32_t n = w * h;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_shards, dim3((n + 255) / 256), dim3(256), 0, stream, recv, shards, stride, w, h, frame);
   return hipGetLastError();
 }
 hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,

@@ -1,7 +1,8 @@
 // main.cpp — `yart` CLI: the reference's `raytracer --scene ...` (main.rs:777-781) on MI355X.
 // Same flags and per-scene defaults (main.rs:78-107, 211-432); the render loop runs through the
 // C ABI of libyart.so. Extensions: --seed (RNG key), --gpus N (pixel blocks dealt round-robin
-// over N devices from one process, summed on the host), --assets DIR (reference input meshes).
+// over N devices from one process and gathered to device 0 with one RCCL gather,
+// yart_render_multi), --assets DIR (reference input meshes).
 // --workers is accepted for compatibility and has no effect on the GPU path.
 #include <chrono>
 #include <cmath>
@@ -10,6 +11,7 @@
 #include <string>
 #include <sys/stat.h>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/yart.h"
@@ -29,6 +31,28 @@ static void mkdirs(const std::string& d) {
     if (i < d.size()) cur += d[i];
   }
 }
+
+// The reference's indicatif bar (main.rs:735-761): "Rendering [elapsed] [bar] pct pos/len px",
+// fed from yart_render's progress callback (on this thread); drawn only on a terminal.
+struct Bar {
+  uint64_t total;
+  bool tty = isatty(2) != 0;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  static void cb(uint64_t px, void* user) { static_cast<Bar*>(user)->draw(px); }
+  void draw(uint64_t px) {
+    if (!tty || total == 0) return;
+    const int w = 28, fill = (int)(w * px / total);
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "\r   Rendering [%7.1fs] [", s);
+    for (int i = 0; i < w; ++i) std::fputc(i < fill ? '=' : (i == fill ? '>' : ' '), stderr);
+    std::fprintf(stderr, "] %3d%% %7llu/%-7llu px", (int)(100 * px / total), (unsigned long long)px,
+                 (unsigned long long)total);
+    std::fflush(stderr);
+  }
+  void finish() {  // finish_and_clear
+    if (tty) std::fprintf(stderr, "\r%*s\r", 90, "");
+  }
+};
 
 static const char kUsage[] =
     "Usage: yart --scene <SCENE> [--output <OUTPUT>] [--width <WIDTH>] [--height <HEIGHT>] "
@@ -70,34 +94,36 @@ int main(int argc, char** argv) {
     return 1;
   }
   int gpus = cli.gpus > 0 ? cli.gpus : 1;
-  if (gpus > ndev) gpus = ndev;
+  if (gpus > ndev) {
+    std::fprintf(stderr, "warning: --gpus %d but only %d device%s visible; using %d\n", gpus, ndev, ndev > 1 ? "s" : "",
+                 ndev);
+    gpus = ndev;
+  }
   const size_t n3 = 3 * (size_t)o.width * o.height;
-  std::vector<std::vector<double>> parts(gpus, std::vector<double>(n3, 0.0));
-  std::vector<int> rcs(gpus, 0);
-  std::vector<std::string> errs(gpus);
-  std::vector<std::thread> th;
-  for (int g = 0; g < gpus; ++g)
-    th.emplace_back([&, g] {
-      yart_scene* s = nullptr;
-      rcs[g] = yart_scene_create(g, yart_preset_desc(preset), &s);
-      if (rcs[g] == YART_OK) {
-        yart_render_params p{o.width, o.height, (uint32_t)o.samples_per_pixel, (uint32_t)o.max_depth, 0x59415254ull,
-                             (uint32_t)g, (uint32_t)gpus, 0, 0};
-        if (cli.seed) p.seed = cli.seed;
-        rcs[g] = yart_render(s, &cam, &p, parts[g].data(), nullptr, nullptr);
-      }
-      if (rcs[g] != YART_OK) errs[g] = yart_last_error();
-      yart_scene_destroy(s);
-    });
-  for (auto& t : th) t.join();
-  for (int g = 0; g < gpus; ++g)
-    if (rcs[g] != YART_OK) {
-      std::fprintf(stderr, "error: device %d: %s\n", g, errs[g].c_str());
-      return 1;
-    }
   std::vector<double> xyz(n3, 0.0);
-  for (int g = 0; g < gpus; ++g)
-    for (size_t i = 0; i < n3; ++i) xyz[i] = xyz[i] + parts[g][i];  // one writer per pixel: exact
+  yart_render_params p{o.width, o.height, (uint32_t)o.samples_per_pixel, (uint32_t)o.max_depth, 0x59415254ull, 0, 1, 0, 0};
+  if (cli.seed) p.seed = cli.seed;
+  Bar bar{(uint64_t)o.width * o.height};
+  int rc;
+  if (cli.gpus > 0) {
+    // --gpus N: one scene per device, shards rendered at once, ONE RCCL gather to device 0
+    std::vector<int> devs(gpus);
+    for (int g = 0; g < gpus; ++g) devs[g] = g;
+    yart_multi* m = nullptr;
+    rc = yart_multi_create(gpus, devs.data(), yart_preset_desc(preset), &m);
+    if (rc == YART_OK) rc = yart_render_multi(m, &cam, &p, xyz.data(), &Bar::cb, &bar);
+    yart_multi_destroy(m);
+  } else {
+    yart_scene* s = nullptr;
+    rc = yart_scene_create(0, yart_preset_desc(preset), &s);
+    if (rc == YART_OK) rc = yart_render(s, &cam, &p, xyz.data(), &Bar::cb, &bar);
+    yart_scene_destroy(s);
+  }
+  bar.finish();
+  if (rc != YART_OK) {
+    std::fprintf(stderr, "error: %s\n", yart_last_error());
+    return 1;
+  }
   std::vector<uint8_t> rgba(4 * (size_t)o.width * o.height);
   if (yart_finalize_rgba8(0, xyz.data(), o.width, o.height, (uint32_t)o.samples_per_pixel, rgba.data()) != YART_OK) {
     std::fprintf(stderr, "error: %s\n", yart_last_error());

@@ -92,6 +92,17 @@ def load_device():
     _sig(L, "yart_intersect", I, P, P, U32, P, P)
     _sig(L, "yart_probe_rng", I, I, U64, U32, U32, U32, P)
     _sig(L, "yart_probe_math", I, I, I, P, P, U32, P)
+    _sig(L, "yart_shard_packed_len", U64, U32, U32, U32, U32)
+    _sig(L, "yart_render_packed_async", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, P)
+    _sig(L, "yart_comm_unique_id", I, P)
+    _sig(L, "yart_comm_init_rank", I, P, I, I, I, C.POINTER(P))
+    _sig(L, "yart_comm_init_all", I, I, P, P)
+    _sig(L, "yart_comm_destroy", None, P)
+    _sig(L, "yart_gather_frame_async", I, P, P, U32, U32, I, P, P)
+    _sig(L, "yart_multi_create", I, I, P, C.POINTER(abi.SceneDesc), C.POINTER(P))
+    _sig(L, "yart_render_multi", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, abi.PROGRESS_FN, P)
+    _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
+    _sig(L, "yart_multi_destroy", None, P)
     _dev = L
     return L
 
@@ -186,10 +197,17 @@ class DeviceScene:
         _check_dev(load_device().yart_scene_get_info(self._s, C.byref(i)))
         return i
 
-    def render(self, cam, params):
+    def render(self, cam, params, progress=None):
+        """Host-output render (yart_render). progress: optional callable(pixels_done), called on
+        this thread while the device works."""
         out = np.zeros((params.height, params.width, 3), dtype=np.float64)
-        _check_dev(load_device().yart_render(self._s, C.byref(cam), C.byref(params), _ptr(out), abi.PROGRESS_FN(0), None))
+        cb = abi.PROGRESS_FN((lambda px, user: progress(px)) if progress else 0)
+        _check_dev(load_device().yart_render(self._s, C.byref(cam), C.byref(params), _ptr(out), cb, None))
         return out
+
+    def render_packed_async(self, cam, params, d_packed_ptr, stream_ptr):
+        _check_dev(load_device().yart_render_packed_async(self._s, C.byref(cam), C.byref(params),
+                                                         C.c_void_p(d_packed_ptr), C.c_void_p(stream_ptr)))
 
     def render_with_stats(self, cam, params):
         out = np.zeros((params.height, params.width, 3), dtype=np.float64)
@@ -229,3 +247,78 @@ def write_png(path, rgba):
     rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
     h, w, _ = rgba.shape
     _check_host(load_host().yart_write_png(str(path).encode(), _ptr(rgba), w, h))
+
+
+def shard_packed_len(width, height, shard_index, shard_count):
+    """Doubles in shard `shard_index`'s block-packed buffer (yart_shard_packed_len)."""
+    return int(load_device().yart_shard_packed_len(width, height, shard_index, shard_count))
+
+
+class Comm:
+    """An RCCL communicator of libyart (yart_comm_init_rank): one rank per process/GPU. The root's
+    128-byte id reaches the other ranks through the caller's own channel (e.g. torch.distributed)."""
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES)()
+        _check_dev(load_device().yart_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid, n_ranks, rank, device):
+        assert len(uid) == abi.COMM_ID_BYTES
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES).from_buffer_copy(uid)
+        self._c = C.c_void_p()
+        _check_dev(load_device().yart_comm_init_rank(buf, n_ranks, rank, device, C.byref(self._c)))
+        self.n_ranks, self.rank, self.device = n_ranks, rank, device
+
+    def gather_frame_async(self, d_packed_ptr, width, height, d_frame_ptr, stream_ptr, root=0):
+        _check_dev(load_device().yart_gather_frame_async(self._c, C.c_void_p(d_packed_ptr), width, height, root,
+                                                        C.c_void_p(d_frame_ptr), C.c_void_p(stream_ptr)))
+
+    def close(self):
+        if self._c:
+            load_device().yart_comm_destroy(self._c)
+            self._c = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiScene:
+    """One process, N devices (yart_multi_create): a scene on each and an RCCL communicator."""
+
+    def __init__(self, desc, devices):
+        L = load_device()
+        owner = desc
+        if hasattr(desc, "desc"):
+            desc = desc.desc
+        devs = (C.c_int * len(devices))(*devices)
+        self._m = C.c_void_p()
+        _check_dev(L.yart_multi_create(len(devices), devs, desc, C.byref(self._m)))
+        del owner
+        self.devices = list(devices)
+
+    def render(self, cam, params, progress=None):
+        out = np.zeros((params.height, params.width, 3), dtype=np.float64)
+        cb = abi.PROGRESS_FN((lambda px, user: progress(px)) if progress else 0)
+        _check_dev(load_device().yart_render_multi(self._m, C.byref(cam), C.byref(params), _ptr(out), cb, None))
+        return out
+
+    def last_timing(self):
+        r, g = C.c_double(), C.c_double()
+        _check_dev(load_device().yart_multi_last_timing(self._m, C.byref(r), C.byref(g)))
+        return r.value, g.value
+
+    def close(self):
+        if self._m:
+            load_device().yart_multi_destroy(self._m)
+            self._m = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -103,7 +103,11 @@ DEVICE_SYMBOLS = [
     "yart_scene_get_info", "yart_camera_init", "yart_render_async", "yart_frame_timing", "yart_render",
     "yart_render_with_stats",
     "yart_finalize_rgba8_async", "yart_finalize_rgba8", "yart_intersect", "yart_probe_rng", "yart_probe_math",
+    "yart_shard_packed_len", "yart_render_packed_async", "yart_comm_unique_id", "yart_comm_init_rank",
+    "yart_comm_init_all", "yart_comm_destroy", "yart_gather_frame_async", "yart_multi_create", "yart_render_multi",
+    "yart_multi_last_timing", "yart_multi_destroy",
 ]
+COMM_ID_BYTES = 128
 HOST_SYMBOLS = [
     "yart_preset_create", "yart_preset_destroy", "yart_preset_desc", "yart_preset_defaults", "yart_preset_stand_in",
     "yart_scene_names", "yart_resolve_dimensions", "yart_cli_parse", "yart_resolve_render_options",

@@ -14,6 +14,16 @@ import numpy as np
 import torch
 
 
+def covered_axis(n):
+    """main.rs:636-647: the 8 crops of width n // 8 start at n * col // 8."""
+    m = np.zeros(n, dtype=bool)
+    cw = n // 8
+    for col in range(8):
+        x0 = n * col // 8
+        m[x0:x0 + cw] = True
+    return m
+
+
 def block_owner(width, height, world):
     """(H, W) int array: the rank that renders each pixel."""
     bx = (width + 7) // 8
@@ -54,4 +64,54 @@ class ShardGather:
             flat = frame.view(-1, self.channels)
             for k in range(self.world):
                 flat.index_copy_(0, self.idx[k], self.recv[k][:self.n[k]])
+        return frame
+
+
+def packed_pixels(width, height, world, rank):
+    """For shard `rank` of `world` in libyart's block-packed layout (yart_shard_packed_len): the
+    frame pixel index (y * W + x) of every slot, -1 for slots outside the frame or the crop grid.
+    Slot s of local block j is pixel (x, y) of global block b = rank + j * world with
+    x = (b % bx) * 8 + s % 8, y = (b // bx) * 8 + s // 8."""
+    bx, by = (width + 7) // 8, (height + 7) // 8
+    blocks = np.arange(rank, bx * by, world)
+    s = np.arange(64)
+    x = (blocks[:, None] % bx) * 8 + s[None, :] % 8
+    y = (blocks[:, None] // bx) * 8 + s[None, :] // 8
+    cx, cy = covered_axis(width), covered_axis(height)
+    ok = (x < width) & (y < height)
+    ok[ok] = cx[x[ok]] & cy[y[ok]]
+    return np.where(ok, y * width + x, -1).reshape(-1)
+
+
+class PackedGather:
+    """The frame gather libyart does natively (yart_gather_frame_async: one ncclGather + unpack
+    kernel), restated over torch.distributed for backends libyart cannot drive (gloo rehearsals
+    on one device, CPU tests): every rank sends its packed shard (equal-sized packets of the
+    largest shard's length), dst scatters them into the frame. Bitwise the native path."""
+
+    def __init__(self, width, height, world, rank, device, dtype=torch.float64, dst=0):
+        self.rank, self.world, self.dst = rank, world, dst
+        self.n_max = len(packed_pixels(width, height, world, 0))  # shard 0 is the largest
+        self.send = torch.zeros((self.n_max, 3), dtype=dtype, device=device)
+        if rank == dst:
+            self.recv = [torch.zeros_like(self.send) for _ in range(world)]
+            self.idx, self.sel = [], []
+            for r in range(world):
+                pix = packed_pixels(width, height, world, r)
+                keep = np.flatnonzero(pix >= 0)
+                self.sel.append(torch.from_numpy(keep).to(device))
+                self.idx.append(torch.from_numpy(pix[keep]).to(device))
+        else:
+            self.recv = None
+
+    def __call__(self, packed, frame, dist, group=None):
+        """`packed`: this rank's packed shard (n * 64 * 3 doubles); on dst `frame` (H, W, 3) gets
+        every covered pixel (uncovered ones are left as they are: zero them once)."""
+        n = min(packed.numel() // 3, self.n_max)
+        self.send[:n].copy_(packed.view(-1, 3)[:n])
+        dist.gather(self.send, self.recv, dst=self.dst, group=group)
+        if self.rank == self.dst:
+            flat = frame.view(-1, 3)
+            for r in range(self.world):
+                flat.index_copy_(0, self.idx[r], self.recv[r].index_select(0, self.sel[r]))
         return frame
