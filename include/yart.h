@@ -221,7 +221,11 @@ typedef struct yart_render_stats {
   uint64_t leaf_visits;    /* QBVH leaves tested (<= 4 triangles each)           */
   uint64_t leaf_tris;      /* triangles tested inside leaves                     */
   uint64_t light_tests;    /* primitive hits re-run by pdf_value (pdf.rs:452)    */
-  uint64_t reserved[9];
+  uint64_t mesh_rewalks;   /* front-to-back QBVH walks redone in reference order */
+  uint64_t coop_rounds;    /* cooperative QBVH walk: wave rounds (16 quad steps)  */
+  uint64_t coop_leaf_rounds; /* ... rounds in which some quad tested a leaf      */
+  uint64_t coop_walks;     /* ... wave-level walks started                       */
+  uint64_t reserved[5];
 } yart_render_stats;
 
 typedef void (*yart_progress_fn)(uint64_t pixels_done, void* user);

@@ -53,7 +53,7 @@ def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False)
         _, c = s.render_with_stats(cam, prm)
         line["counts"] = {"samples": c.samples, "segments": c.segments, "prim_tests": c.prim_tests,
                           "node_visits": c.node_visits, "leaf_visits": c.leaf_visits, "leaf_tris": c.leaf_tris,
-                          "light_tests": c.light_tests}
+                          "light_tests": c.light_tests, "mesh_rewalks": c.mesh_rewalks, "coop_rounds": c.coop_rounds, "coop_leaf_rounds": c.coop_leaf_rounds, "coop_walks": c.coop_walks}
         info = s.info()
         if info.bvh_nodes:
             # algorithmic bytes of the traversal: 128 B per inner node visit,

@@ -14,11 +14,12 @@ run() {
 STEPS=${STEPS:-"pytest smoke bench"}
 for s in $STEPS; do
   case $s in
-    pytest) run pytest 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 150 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 150 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
     smoke)  run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
     rehearse) YART_BENCH_SAME_DEVICE=1 run rehearse 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 2 --warmup 1 --no-stats --cpu-spp 0 ;;
-    configs) run configs 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ;;
+    configs) run configs 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
+    configs_ref) YART_MESH_WALK=ref run configs_ref 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
   esac
 done

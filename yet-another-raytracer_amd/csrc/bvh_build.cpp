@@ -74,6 +74,9 @@ struct Builder {
       const double* nn = &normals[9 * (size_t)perm[off + i]];
       for (int c = 0; c < 9; ++c) out->normals[9 * (size_t)(off + i) + c] = nn[c];
     }
+    LeafAux a{};
+    for (int k = 0; k < 3; ++k) { a.lo[k] = (float)b.mn[k]; a.hi[k] = (float)b.mx[k]; }  // exact: f32 corners
+    out->aux.push_back(a);
     return {true, b, (1u << 31) | (n << 27) | li};
   }
 
@@ -99,8 +102,8 @@ struct Builder {
         mn[a] = ch[k]->has ? (float)ch[k]->box.mn[a] : INFINITY;
         mx[a] = ch[k]->has ? (float)ch[k]->box.mx[a] : INFINITY;
       }
-      node.lo[k][0] = mn[0]; node.lo[k][1] = mn[1]; node.lo[k][2] = mn[2]; node.lo[k][3] = mx[0];
-      node.hi[k][0] = mx[1]; node.hi[k][1] = mx[2];
+      node.lo[k][0] = mn[0]; node.lo[k][1] = mx[0]; node.lo[k][2] = mn[1]; node.lo[k][3] = mx[1];
+      node.hi[k][0] = mn[2]; node.hi[k][1] = mx[2];
       std::memcpy(&node.hi[k][2], &ch[k]->id, 4);
       uint32_t code = 0;  // this child's push rank for each of the 8 ray octants, 2 bits each
       for (uint32_t pos = 0; pos < 8; ++pos) {
@@ -116,6 +119,32 @@ struct Builder {
     return {true, merge(lb, rb), (uint32_t)(out->nodes.size() - 1)};
   }
 };
+
+// Depth-first visit order of the leaves for one ray octant, as L4QBVH::hit walks them
+// (qbvh.rs:520-531): a node's hit children are pushed in ORDER_TABLE order and popped last-first,
+// so siblings are visited in descending push rank. Pruning only removes subtrees; it never
+// reorders, so this rank orders any two leaves the reference visits for a ray of that octant.
+void rank_leaves(BuiltMesh& m, uint32_t root) {
+  for (uint32_t pos = 0; pos < 8; ++pos) {
+    uint32_t next = 0;
+    std::vector<uint32_t> stack{root};
+    while (!stack.empty()) {
+      const uint32_t id = stack.back();
+      stack.pop_back();
+      if (id >> 31) { m.aux[id & ((1u << 27) - 1u)].rank[pos] = next++; continue; }
+      const DevNode& nd = m.nodes[id];
+      uint32_t by_rank[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      for (int k = 0; k < 4; ++k) {
+        uint32_t child, code;
+        std::memcpy(&child, &nd.hi[k][2], 4);
+        std::memcpy(&code, &nd.hi[k][3], 4);
+        by_rank[(code >> (2 * pos)) & 3u] = child;
+      }
+      for (int r = 0; r < 4; ++r)  // pushed lowest rank first: the highest rank is popped (visited) first
+        if (by_rank[r] != 0xFFFFFFFFu) stack.push_back(by_rank[r]);
+    }
+  }
+}
 
 }  // namespace
 
@@ -150,7 +179,10 @@ bool build_qbvh(uint32_t n, const float* positions, const double* normals, Built
     b.tri_box[t] = bx;
   }
   out.normals.assign(9 * (size_t)n, 0.0);
+  out.extent = 0.0f;  // max |coordinate| of the mesh (the f32 box test's error scale)
+  for (size_t i = 0; i < 9 * (size_t)n; ++i) out.extent = std::max(out.extent, std::fabs(positions[i]));
   b.construct(0, n, 0, normals);
+  rank_leaves(out, (uint32_t)out.nodes.size() - 1);
   if (3 * out.depth + 1 > (uint32_t)kStackSlots) {
     err = "QBVH too deep for the device traversal stack (depth " + std::to_string(out.depth) + ")";
     return false;

@@ -12,7 +12,9 @@ struct BuiltMesh {
   std::vector<DevNode> nodes;       // post-order; root = nodes.back()
   std::vector<float> leaves;        // kLeafFloats per leaf (see DevNode)
   std::vector<double> normals;      // 9 per sorted triangle
+  std::vector<LeafAux> aux;         // per leaf: box + reference traversal rank per ray octant
   uint32_t depth = 0;               // inner-node levels on the deepest path
+  float extent = 0.0f;              // max |vertex coordinate|
 };
 
 // L4QBVH::new (qbvh.rs:252-361): recursive median split into four children per node, <= 4

@@ -254,8 +254,14 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
     HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
     HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
+    // YART_MESH_WALK=ref: walk every ray in the reference's order (A/B and tests); default:
+    // front to back with the exact fallback (kernels.hip qbvh_coop)
+    const char* walk = std::getenv("YART_MESH_WALK");
+    if (!(walk && std::strcmp(walk, "ref") == 0))
+      HIP_TRY(upload(s->owned, b.aux.data(), b.aux.size(), &dm[m].aux, bytes), "upload leaf records");
     dm[m].root = (uint32_t)b.nodes.size() - 1;
     dm[m].n_nodes = (uint32_t)b.nodes.size();
+    dm[m].extent = b.extent;
   }
   HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
   if (use_world) {
@@ -640,8 +646,8 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
   HIP_TRY(hipMemsetAsync(d_out, 0, bytes, stream), "hipMemset");
   if (stats) {
-    HIP_TRY(hipMalloc(&d_stats, 8 * sizeof(unsigned long long)), "hipMalloc stats");
-    HIP_TRY(hipMemsetAsync(d_stats, 0, 8 * sizeof(unsigned long long), stream), "hipMemset");
+    HIP_TRY(hipMalloc(&d_stats, 12 * sizeof(unsigned long long)), "hipMalloc stats");
+    HIP_TRY(hipMemsetAsync(d_stats, 0, 12 * sizeof(unsigned long long), stream), "hipMemset");
   }
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
@@ -660,12 +666,14 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   if (int rc = wait_with_progress({done}, {s->device}, {&pr}, pr.pixels, progress, user)) return rc;
   HIP_TRY(hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, stream), "copy output");
   if (stats) {
-    unsigned long long v[8];
+    unsigned long long v[12];
     HIP_TRY(hipMemcpyAsync(v, d_stats, sizeof v, hipMemcpyDeviceToHost, stream), "copy stats");
     HIP_TRY(hipStreamSynchronize(stream), "copy stats");
     std::memset(stats, 0, sizeof *stats);
     stats->samples = v[0]; stats->segments = v[1]; stats->prim_tests = v[2]; stats->node_visits = v[3];
     stats->leaf_visits = v[4]; stats->leaf_tris = v[5]; stats->light_tests = v[6];
+    stats->mesh_rewalks = v[7];
+    stats->coop_rounds = v[8]; stats->coop_leaf_rounds = v[9]; stats->coop_walks = v[10];
   }
   HIP_TRY(hipStreamSynchronize(stream), "copy output");
   return ok();

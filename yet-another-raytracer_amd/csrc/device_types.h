@@ -48,8 +48,8 @@ struct DevTexture {
 };
 
 // Child k of a node is two float4s, read by lane k of a quad in the cooperative traversal (one
-// 64-B load per quad per float4 row): lo[k] = (min x, min y, min z, max x), hi[k] = (max y,
-// max z, child id bits, push ranks). The push rank of child k for ray octant o (bits 2o..2o+1) is
+// 64-B load per quad per float4 row): lo[k] = (min x, max x, min y, max y), hi[k] = (min z,
+// max z, child id bits, push ranks) — each axis's slab as an adjacent (min, max) pair. The push rank of child k for ray octant o (bits 2o..2o+1) is
 // its position in the ORDER_TABLE row of the node's split axes (qbvh.rs:14-31), precomputed so a
 // lane needs one shift instead of the table walk. Empty children have +inf boxes (QBVHNode::new,
 // qbvh.rs:570-572).
@@ -62,12 +62,26 @@ static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
 // sorted triangle index (bits), 2 pad. Lane k of a quad reads record k.
 constexpr int kLeafFloats = 48;
 
+// Per-leaf side record for the front-to-back walk (qbvh_coop): the leaf's box exactly as its
+// parent stores it, and the leaf's position in the reference's traversal order for each of the
+// 8 ray octants (the depth-first order ORDER_TABLE gives, qbvh.rs:14-31, 520-531): the tie rule
+// between equal-t hits in different leaves, and the box re-test that decides whether the
+// front-to-back result is provably the reference's (kernels.hip, qbvh_coop).
+struct alignas(16) LeafAux {
+  float lo[3], hi[3];
+  uint32_t pad[2];
+  uint32_t rank[8];
+};
+static_assert(sizeof(LeafAux) == 64, "LeafAux must be 64 B");
+
 struct DevMesh {
   const DevNode* nodes;
   const float* leaves;        // kLeafFloats per leaf (see DevNode)
   const double* normals;      // 9 per sorted triangle: n0 n1 n2
+  const LeafAux* aux;         // per leaf; null = walk in the reference's order only
   uint32_t root;              // the last node pushed (qbvh.rs:384)
   uint32_t n_nodes;
+  float extent;               // max |vertex coordinate| (error scale of the f32 box test)
 };
 
 // World BVH over the object list (not in the reference, whose HittableList is a linear scan):

@@ -686,8 +686,9 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
 }
 
 // --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543)
-struct Stats { unsigned long long v[8]; };
-enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };
+constexpr int kNumStats = 12;
+struct Stats { unsigned long long v[kNumStats]; };
+enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };  // ST_REWALK = 7 below
 
 // Ray octant: x >= 0 | y >= 0 << 1 | z >= 0 << 2, the ORDER_TABLE column (qbvh.rs:14-31); a
 // child's push rank for it is 2 bits of its node record (bvh_build.cpp).
@@ -706,7 +707,7 @@ __device__ __forceinline__ float4 ld4(gfloat4p p, size_t i) {
 // One child's slab test in f64 on its f32 box (AABB::hit as qbvh.rs:430-470 evaluates it per lane).
 __device__ __forceinline__ bool child_hit(float4 lo, float4 hi, const double ro[3], const double inv[3], double tmin,
                                           double tmax) {
-  const float bmn[3] = {lo.x, lo.y, lo.z}, bmx[3] = {lo.w, hi.x, hi.y};
+  const float bmn[3] = {lo.x, lo.z, hi.x}, bmx[3] = {lo.y, lo.w, hi.y};  // DevNode: (min, max) per axis
   double l = tmin, h = tmax;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -794,18 +795,45 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
 // child k of an inner node (the QBVH's 4-wide box test, qbvh.rs:430-470, as 4 lanes) or
 // triangle k of a leaf (hitx4, qbvh.rs:475-540). The wave's rays are staged in LDS and handed
 // to quads as they finish (16 quads, a ballot per round), so the wave's cost is its rays' total
-// step count / 16 rather than 64 x its slowest ray. Per ray the node order, the t_max used at
-// each test and the tie rule are the per-lane walk's: the leaf's winner is the smallest t among
-// its hits with the lowest index on ties — what the sequential strict `t_max > t` loop keeps.
-// Call from converged code (all 64 lanes); `want` selects the lanes that have a ray.
+// step count / 16 rather than 64 x its slowest ray. Call from converged code (all 64 lanes);
+// `want` selects the lanes that have a ray.
+//
+// Two visiting orders, one result.
+//  * Reference order (qbvh.rs:381-543 as written): children pushed in ORDER_TABLE order, the box
+//    test against the running t_max, a leaf hit kept only if strictly nearer. For a positive
+//    direction component the table walks far children first, so little is pruned.
+//  * Front to back (default when the mesh has LeafAux records): nearest child first, pruned
+//    against the best hit so far. Its answer is W = the minimum over the candidate set
+//    S = {triangles that pass Möller–Trumbore with t_min <= t < t_max_in, in a leaf whose box passes
+//    the slab test at t_max_in} under the order (t, reference depth-first leaf rank, lane). The
+//    reference's answer is W too whenever t_W >= l(leaf box of W) (the f64 slab entry the
+//    reference computes for it): then every ancestor of W passes its box test at any t_max > t_W
+//    (slab entries of nested f32 boxes are monotone: rounding is monotone), so the reference
+//    reaches W while its t_max > t_W and keeps it, and every triangle it keeps lies in S, so nothing
+//    it meets afterwards is strictly nearer. That condition is re-checked exactly at the end of
+//    every front-to-back walk (one 64-B load); a ray that fails it — W's t rounded to before its
+//    own box entry — walks again in the reference order. Pruning keeps equal-t candidates (a
+//    child is tested against min(t_max_in, t_best (1 + 2^-8)), a popped entry dropped only if its
+//    entry exceeds that), so W is always visited unless a triangle's computed t lies more than
+//    2^-8 relative before its box's computed entry (a Möller–Trumbore condition number above
+//    ~2^44: a ray within ~1e-13 rad of the triangle's plane). Rays with a zero, NaN or infinite
+//    direction or origin component, where the monotonicity argument does not hold, walk in the
+//    reference order from the start.
 struct CoopRay { double o[3], d[3], inv[3], tmax; };  // result: o = (t, u, v), d[0] = found << 32 | tri
 constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
-constexpr int kCoopBytes = kCoopRayBytes + kStackSlots * 16 * 4;  // + per-quad stacks [slot][quad]
-static_assert(kCoopBytes <= kStackSlots * 64 * 4, "cooperative walk must fit the wave's stack region");
+constexpr int kCoopSlots = kStackSlots;  // per quad: node id + its f32 box entry
+constexpr int kCoopBytes = kCoopRayBytes + kCoopSlots * 16 * 8;
+// LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
+constexpr int kWaveLdsWords = (kCoopBytes / 4 > kStackSlots * 64) ? kCoopBytes / 4 : kStackSlots * 64;
+constexpr double kF2bMargin = 0x1p-8;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float x) {
+  return __uint_as_float(quad_perm<CTRL>(__float_as_uint(x)));
 }
 template <int CTRL>
 __device__ __forceinline__ double quad_perm(double x) {
@@ -822,6 +850,46 @@ __device__ __forceinline__ void quad_min(double& t, uint32_t& key) {
   t = other ? ot : t;
   key = other ? ok : key;
 }
+// One child's slab test as child_hit, also returning its entry l.
+__device__ __forceinline__ bool child_hit_l(float4 lo, float4 hi, const double ro[3], const double inv[3], double tmin,
+                                            double tmax, double& l) {
+  const float bmn[3] = {lo.x, lo.z, hi.x}, bmx[3] = {lo.y, lo.w, hi.y};  // DevNode: (min, max) per axis
+  double h = tmax;
+  l = tmin;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double t0 = ((double)bmn[j] - ro[j]) * inv[j], t1 = ((double)bmx[j] - ro[j]) * inv[j];
+    l = fmax(l, fmin(t0, t1));
+    h = fmin(h, fmax(t0, t1));
+  }
+  return h > l;
+}
+// Conservative f32 slab test for the front-to-back walk. The ray's constants (take() in
+// qbvh_coop): inv32 = (float)(1/d), and per axis c = (-o/d -+ s·delta, -o/d +- s·delta) with
+// s = sign(1/d) and delta = 2^-20 (mesh extent + max|o|) |1/d|, so that t0 = fma(min, inv32, c.x) is
+// the axis's entry lowered by delta and t1 = fma(max, inv32, c.y) its exit raised by delta
+// whatever the sign of d. Every f32 rounding here (inv32, o/d, the fma) is below 2^-24 (extent
+// + |o|) |1/d| < delta / 5, so [l, h] contains the reference's f64 interval, and t_min / t_max come
+// in rounded outward: whenever the f64 test (h > l) passes, this one (h >= l) passes — it visits a
+// superset of nodes, which the front-to-back walk allows (qbvh_coop) — at half the VALU cost of
+// f64 arithmetic, two axis bounds per packed fma.
+typedef float vfloat2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool child_hit_f32(float4 lo, float4 hi, const float inv32[3], const vfloat2 c[3],
+                                              float tmin32, float tmax32, float& l) {
+  const vfloat2 bx = {lo.x, lo.y}, by = {lo.z, lo.w}, bz = {hi.x, hi.y};
+  const vfloat2 tx = __builtin_elementwise_fma(bx, (vfloat2)(inv32[0]), c[0]);
+  const vfloat2 ty = __builtin_elementwise_fma(by, (vfloat2)(inv32[1]), c[1]);
+  const vfloat2 tz = __builtin_elementwise_fma(bz, (vfloat2)(inv32[2]), c[2]);
+  l = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), tmin32));
+  const float h = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tmax32));
+  return h >= l;
+}
+// Rank of this lane's key among the quad's (ties to the lower lane); +inf keys rank last.
+__device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
+  const float k1 = quad_perm<0xB1>(key), k2 = quad_perm<0x4E>(key), k3 = quad_perm<0x1B>(key);
+  return (uint32_t)((k1 < key) | ((k1 == key) & ((c ^ 1u) < c))) + (uint32_t)((k2 < key) | ((k2 == key) & ((c ^ 2u) < c))) +
+         (uint32_t)((k3 < key) | ((k3 == key) & ((c ^ 3u) < c)));
+}
 #ifndef YART_COOP_LEAF_MIN
 #define YART_COOP_LEAF_MIN 1  // quads waiting at a leaf before a round runs the leaf branch
 #endif
@@ -831,6 +899,7 @@ __device__ __forceinline__ void quad_min(double& t, uint32_t& key) {
 #else
 #define YART_COOP_ATTR __forceinline__  // inlined: +4% david, +11% bunny over a call (caller spills)
 #endif
+enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // per wave: lane 0 counts
 template <bool STATS>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
@@ -841,6 +910,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
+  float* qent = reinterpret_cast<float*>(lds + kCoopRayBytes + kCoopSlots * 16 * 4);
   const uint32_t n = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   if (want) {
@@ -854,28 +924,64 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
+  const __attribute__((address_space(1))) LeafAux* aux = (const __attribute__((address_space(1))) LeafAux*)M.aux;
   const uint32_t root = M.root;
+  const float extent = M.extent;
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
-  double ro[3], rd[3], inv[3], tmax = 0.0, bt = 0.0, bu = 0.0, bv = 0.0;
-  uint32_t pos = 0, node = 0, btri = 0, win = 0;  // win: the quad lane holding the best hit
+  // The best hit so far is written to the ray's LDS record by the lane that found it (the
+  // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
+  double ro[3], rd[3], inv[3], tin = 0.0, tb = 0.0, teff = 0.0;
+  float inv32[3], tmin32 = 0.0f, teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
+  vfloat2 c32[3];
+  float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
+  uint32_t pos = 0, node = 0, bleaf = 0;
   int cursor = 0;
-  bool fnd = false;
-  auto take = [&]() {
-    const CoopRay& s = rays[ray];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) { ro[j] = s.o[j]; rd[j] = s.d[j]; inv[j] = s.inv[j]; }
-    tmax = s.tmax;
-    pos = ray_octant(rd);
+  bool fnd = false, f2b = false;
+  auto restart = [&](bool front_to_back) {
     node = root;
     cursor = 0;
     fnd = false;
-    win = 0;
+    tb = tin;    // best so far (reference order: the running t_max)
+    teff = tin;  // the t_max child boxes are tested against
+    teff32 = (float)(tin + fabs(tin) * 0x1p-20);
+    bound = INFINITY;
+    f2b = front_to_back;
+  };
+  auto take = [&]() {
+    const CoopRay& s = rays[ray];
+    bool ok = aux != nullptr && extent < 1e15f;
+    double O = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      ro[j] = s.o[j]; rd[j] = s.d[j]; inv[j] = s.inv[j];
+      // front to back needs finite, non-zero direction components (the slab entries of nested
+      // boxes are then monotone) and magnitudes the f32 test holds without overflow
+      ok = ok && rd[j] != 0.0 && fabs(ro[j]) < 1e15 && fabs(inv[j]) < 1e15;
+      O = fmax(O, fabs(ro[j]));
+    }
+    const double m = ((double)extent + O) * 0x1p-20;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double a = -(ro[j] * inv[j]), dl = inv[j] > 0.0 ? m * inv[j] : -(m * inv[j]);
+      const double sd = inv[j] > 0.0 ? dl : -dl;
+      inv32[j] = (float)inv[j];
+      c32[j] = vfloat2{(float)(a - sd), (float)(a + sd)};
+    }
+    tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
+    tin = s.tmax;
+    pos = ray_octant(rd);
+    restart(ok);
   };
   if (ray < n) take();
+  if (STATS && lane == 0) st.v[ST_WALKS]++;
   for (;;) {
     const bool has = ray < n;
     if (__ballot(has) == 0) break;
+    if (STATS && lane == 0) {
+      st.v[ST_ROUNDS]++;
+      st.v[ST_LEAF_ROUNDS] += __ballot(has && (node >> 31)) != 0 ? 1u : 0u;
+    }
     bool fin = false;
 #if YART_COOP_LEAF_MIN > 1
     // Leaf rounds wait until enough quads sit at a leaf (or none can descend): a round pays for
@@ -899,7 +1005,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
                        "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y));
           double tt, uu, vv;
-          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tmax, tt, uu, vv)) {
+          // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
+          // back: the tie goes to the reference's visiting order below)
+          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tin, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
             t = tt; u = uu; v = vv; key = c; id = __float_as_uint(p2.y);
           }
         }
@@ -907,16 +1015,45 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
         quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
         quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
         if (key < 4u) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
-          tmax = t; fnd = true; win = key;
-          if (c == key) { bt = t; bu = u; bv = v; btri = id; }
+          // t == tb only front to back with a best already held (t < t_max_in): the leaf the
+          // reference visits first keeps it (different leaves; in one leaf the lower lane won above)
+          const bool better = t < tb || aux[li].rank[pos] < aux[bleaf].rank[pos];
+          if (better) {
+            tb = t; fnd = true; bleaf = li;
+            if (c == key) {
+              CoopRay& s = rays[ray];
+              s.o[0] = t; s.o[1] = u; s.o[2] = v;
+              s.d[0] = __longlong_as_double((long long)((1ull << 32) | id));
+            }
+            if (f2b) {
+              const double lim = t * (1.0 + kF2bMargin);
+              teff = lim < tin ? lim : tin;
+              teff32 = (float)(teff + teff * 0x1p-20);
+              bound = (float)lim;
+            } else {
+              teff = t;
+            }
+          }
         }
       } else {
         const gfloat4p N = nodes + 8 * (size_t)node;
         const float4 lo = ld4(N, c);
         float4 hi = ld4(N, 4 + c);
         asm volatile("" : "+v"(hi.z), "+v"(hi.w));  // child id and ranks with the box, one round
-        const bool hk = child_hit(lo, hi, ro, inv, tmin, tmax);
-        const uint32_t rk = (__float_as_uint(hi.w) >> (2u * pos)) & 3u;
+        bool hk;
+        float ent;
+        if (f2b) {
+          hk = child_hit_f32(lo, hi, inv32, c32, tmin32, teff32, ent);
+          ent = fminf(ent, 3.0e38f);
+        } else {
+          double l;
+          hk = child_hit_l(lo, hi, ro, inv, tmin, teff, l);
+          ent = 0.0f;  // unused in the reference order
+        }
+        // push rank: reference order from ORDER_TABLE (precomputed per octant); front to back
+        // 3 - (distance rank), so the nearest hit child is the one taken next and the farthest
+        // sits deepest in the stack
+        const uint32_t rk = f2b ? 3u - quad_rank(hk ? ent : INFINITY, c) : (__float_as_uint(hi.w) >> (2u * pos)) & 3u;
         uint32_t ordered = hk ? 1u << rk : 0u;  // bit r: the child of push rank r was hit
         ordered |= quad_perm<0xB1>(ordered);
         ordered |= quad_perm<0x4E>(ordered);
@@ -929,26 +1066,43 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           uint32_t nx = (hk && rk == last) ? child : 0u;
           nx |= quad_perm<0xB1>(nx);
           nx |= quad_perm<0x4E>(nx);
-          if (hk && rk != last) qstk[(cursor + (int)__popc(ordered & ((1u << rk) - 1u))) * 16 + (int)q] = child;
+          if (hk && rk != last) {
+            const int slot = (cursor + (int)__popc(ordered & ((1u << rk) - 1u))) * 16 + (int)q;
+            qstk[slot] = child;
+            qent[slot] = ent;
+          }
           cursor += (int)__popc(ordered) - 1;
           node = nx;
           popped = true;
         }
       }
       if (!popped) {
-        if (cursor == 0) {
-          fin = true;
-        } else {
+        for (;;) {  // front to back: entries whose box begins beyond the bound are dropped
+          if (cursor == 0) { fin = true; break; }
           cursor -= 1;
           node = qstk[cursor * 16 + (int)q];
+          if (!f2b || !(qent[cursor * 16 + (int)q] > bound)) break;
+        }
+      }
+      if (fin && f2b && fnd) {
+        // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
+        // (the f32 test visits a superset) and W's t is not before that box's entry (above)
+        const auto& A = aux[bleaf];
+        double l = tmin, h = tin;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double t0 = ((double)A.lo[j] - ro[j]) * inv[j], t1 = ((double)A.hi[j] - ro[j]) * inv[j];
+          l = fmax(l, fmin(t0, t1));
+          h = fmin(h, fmax(t0, t1));
+        }
+        if (!(h > l && tb >= l)) {
+          if (STATS && c == 0) st.v[ST_REWALK]++;
+          restart(false);
+          fin = false;
         }
       }
     }
-    if (fin && c == (fnd ? win : 0u)) {
-      CoopRay& s = rays[ray];
-      s.o[0] = bt; s.o[1] = bu; s.o[2] = bv;
-      s.d[0] = __longlong_as_double((long long)(fnd ? ((1ull << 32) | btri) : 0ull));
-    }
+    if (fin && !fnd && c == 0) rays[ray].d[0] = 0.0;  // no hit (a hit's record is already written)
     const uint64_t fm = __ballot(fin && c == 0);
     if (fm) {
       if (fin) {
@@ -1538,7 +1692,7 @@ __device__ unsigned long long g_occ[32];
 
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
 __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
-  __shared__ uint32_t s_stack[(HAS_MESH || BVH) ? 4 * kStackSlots * 64 : 1];
+  __shared__ uint32_t s_stack[HAS_MESH ? 4 * kWaveLdsWords : BVH ? 4 * kStackSlots * 64 : 1];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
   // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
@@ -1555,10 +1709,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
-  uint32_t* stk = &s_stack[(HAS_MESH || BVH) ? (wave * kStackSlots * 64 + lane) : 0];
-  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kStackSlots * 64 : 0]);
+  uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
   Stats st;
-  if (STATS) for (int i = 0; i < 8; ++i) st.v[i] = 0;
+  if (STATS) for (int i = 0; i < kNumStats; ++i) st.v[i] = 0;
 
   uint32_t pixel = y * W + x;
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
@@ -1845,7 +1999,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   if (!DYN && A.progress && lane == 0)
     __hip_atomic_store(A.progress, A.progress_base + (blockIdx.x + 1u) * 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (STATS) {
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < kNumStats; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
   }
 }
@@ -1893,7 +2047,7 @@ __global__ __launch_bounds__(256) void k_unpack_shards(const double* __restrict_
 // ------------------------------------------------------------------- batched closest hit
 __global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
                                                    double* __restrict__ hits, int32_t* __restrict__ obj) {
-  __shared__ uint32_t s_stack[4 * kStackSlots * 64];
+  __shared__ uint32_t s_stack[4 * kWaveLdsWords];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const bool active = i < n;  // no early exit: the mesh walk needs the whole wave
@@ -1902,8 +2056,8 @@ __global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevSc
   Hit h;
   int32_t which = -1;
   Stats st;
-  uint32_t* stk = &s_stack[wave * kStackSlots * 64 + lane];
-  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kStackSlots * 64]);
+  uint32_t* stk = &s_stack[wave * kWaveLdsWords + lane];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kWaveLdsWords]);
   const QueryCtx qc{0u, 0u, 0u, i, 0u};  // a medium's draw for query i: seed 0, sample 0, pixel i
   bool hit = false;
   if (S.world_nodes) {

@@ -74,7 +74,9 @@ class SceneInfo(C.Structure):
 class RenderStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("leaf_tris", C.c_uint64),
-                ("light_tests", C.c_uint64), ("reserved", C.c_uint64 * 9)]
+                ("light_tests", C.c_uint64), ("mesh_rewalks", C.c_uint64),
+                ("coop_rounds", C.c_uint64), ("coop_leaf_rounds", C.c_uint64), ("coop_walks", C.c_uint64),
+                ("reserved", C.c_uint64 * 5)]
 
 
 class RenderDefaults(C.Structure):
