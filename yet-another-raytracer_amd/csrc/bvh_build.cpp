@@ -62,22 +62,19 @@ struct Builder {
   Result leaf(uint32_t off, uint32_t n, const double* normals) {
     Box b = tri_box[perm[off]];
     for (uint32_t i = 1; i < n; ++i) b = merge(b, tri_box[perm[off + i]]);
-    uint32_t li = (uint32_t)(out->leaves.size() / kLeafFloats);
-    size_t base = out->leaves.size();
-    out->leaves.resize(base + kLeafFloats, 0.0f);
-    for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t li = (uint32_t)out->aux.size();
+    for (uint32_t i = 0; i < n; ++i) {  // triangle records in sorted order: leaf = [off, off + n)
       const float* v = &pos[9 * (size_t)perm[off + i]];
-      float* rec = &out->leaves[base + 12 * i];
+      float* rec = &out->leaves[kTriFloats * (size_t)(off + i)];
       for (int c = 0; c < 9; ++c) rec[c] = v[c];
-      const uint32_t tri = off + i;  // sorted index: the row of the normal table
-      std::memcpy(&rec[9], &tri, 4);
+      std::memcpy(&rec[9], &li, 4);  // the leaf's index (LeafAux)
       const double* nn = &normals[9 * (size_t)perm[off + i]];
       for (int c = 0; c < 9; ++c) out->normals[9 * (size_t)(off + i) + c] = nn[c];
     }
     LeafAux a{};
     for (int k = 0; k < 3; ++k) { a.lo[k] = (float)b.mn[k]; a.hi[k] = (float)b.mx[k]; }  // exact: f32 corners
     out->aux.push_back(a);
-    return {true, b, (1u << 31) | (n << 27) | li};
+    return {true, b, (1u << 31) | (n << 27) | off};
   }
 
   Result construct(uint32_t off, uint32_t n, uint32_t level, const double* normals) {  // qbvh.rs:253-347
@@ -131,7 +128,12 @@ void rank_leaves(BuiltMesh& m, uint32_t root) {
     while (!stack.empty()) {
       const uint32_t id = stack.back();
       stack.pop_back();
-      if (id >> 31) { m.aux[id & ((1u << 27) - 1u)].rank[pos] = next++; continue; }
+      if (id >> 31) {
+        uint32_t li;
+        std::memcpy(&li, &m.leaves[kTriFloats * (size_t)(id & ((1u << 27) - 1u)) + 9], 4);
+        m.aux[li].rank[pos] = next++;
+        continue;
+      }
       const DevNode& nd = m.nodes[id];
       uint32_t by_rank[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
       for (int k = 0; k < 4; ++k) {
@@ -179,6 +181,7 @@ bool build_qbvh(uint32_t n, const float* positions, const double* normals, Built
     b.tri_box[t] = bx;
   }
   out.normals.assign(9 * (size_t)n, 0.0);
+  out.leaves.assign(kTriFloats * (size_t)n, 0.0f);
   out.extent = 0.0f;  // max |coordinate| of the mesh (the f32 box test's error scale)
   for (size_t i = 0; i < 9 * (size_t)n; ++i) out.extent = std::max(out.extent, std::fabs(positions[i]));
   b.construct(0, n, 0, normals);

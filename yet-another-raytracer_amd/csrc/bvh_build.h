@@ -10,7 +10,7 @@ namespace yart_dev {
 
 struct BuiltMesh {
   std::vector<DevNode> nodes;       // post-order; root = nodes.back()
-  std::vector<float> leaves;        // kLeafFloats per leaf (see DevNode)
+  std::vector<float> leaves;        // kTriFloats per triangle, sorted order (see DevNode)
   std::vector<double> normals;      // 9 per sorted triangle
   std::vector<LeafAux> aux;         // per leaf: box + reference traversal rank per ray octant
   uint32_t depth = 0;               // inner-node levels on the deepest path

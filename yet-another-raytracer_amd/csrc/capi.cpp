@@ -212,7 +212,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     std::string err;
     if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err)) return fail(YART_ERR_UNSUPPORTED, err);
     nodes += (uint32_t)built[m].nodes.size();
-    leaves += (uint32_t)(built[m].leaves.size() / kLeafFloats);
+    leaves += (uint32_t)built[m].aux.size();
     depth = std::max(depth, built[m].depth);
   }
 
@@ -253,7 +253,16 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     BuiltMesh& b = built[m];
     HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
     HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
-    HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
+    // Normals from the OBJ's vn lines are f32 values (tobj parses f32): then an f32 table holds them
+    // exactly in half the bytes (read once per mesh hit, mesh_rec); computed face normals are f64.
+    std::vector<float> n32(b.normals.size());
+    bool exact32 = true;
+    for (size_t i = 0; i < b.normals.size() && exact32; ++i) {
+      n32[i] = (float)b.normals[i];
+      exact32 = (double)n32[i] == b.normals[i];
+    }
+    if (exact32) HIP_TRY(upload(s->owned, n32.data(), n32.size(), &dm[m].normals32, bytes), "upload normals");
+    else HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
     // YART_MESH_WALK=ref: walk every ray in the reference's order (A/B and tests); default:
     // front to back with the exact fallback (kernels.hip qbvh_coop)
     const char* walk = std::getenv("YART_MESH_WALK");

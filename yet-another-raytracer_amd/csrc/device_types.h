@@ -58,9 +58,11 @@ struct alignas(16) DevNode {
   float hi[4][4];  // [k][2]: inner: node index; leaf: 1<<31 | count<<27 | leaf index; [k][3]: ranks
 };
 static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
-// A leaf is 4 triangle records of 12 floats (48 B, three float4s): v0 v1 v2 (x y z each), the
-// sorted triangle index (bits), 2 pad. Lane k of a quad reads record k.
-constexpr int kLeafFloats = 48;
+// Triangle records, 12 floats (48 B, three float4s) each, in the builder's sorted order: v0 v1 v2
+// (x y z each), the index of the leaf holding it (LeafAux), 2 pad. A leaf is the run
+// [first, first + count) its node id names (1<<31 | count<<27 | first); lane k of a quad reads
+// record first + k, and first + k is also the row of the normal table.
+constexpr int kTriFloats = 12;
 
 // Per-leaf side record for the front-to-back walk (qbvh_coop): the leaf's box exactly as its
 // parent stores it, and the leaf's position in the reference's traversal order for each of the
@@ -76,8 +78,9 @@ static_assert(sizeof(LeafAux) == 64, "LeafAux must be 64 B");
 
 struct DevMesh {
   const DevNode* nodes;
-  const float* leaves;        // kLeafFloats per leaf (see DevNode)
-  const double* normals;      // 9 per sorted triangle: n0 n1 n2
+  const float* leaves;        // kTriFloats per sorted triangle (see DevNode)
+  const double* normals;      // 9 per sorted triangle: n0 n1 n2 (null when normals32 holds them)
+  const float* normals32;     // the same in f32 when every value is exactly an f32 (OBJ vn)
   const LeafAux* aux;         // per leaf; null = walk in the reference's order only
   uint32_t root;              // the last node pushed (qbvh.rs:384)
   uint32_t n_nodes;

@@ -754,8 +754,8 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
   for (;;) {
     const uint32_t id = stk[cursor * 64];
     if (id >> 31) {
-      const uint32_t count = (id >> 27) & 0xFu, li = id & ((1u << 27) - 1u);
-      const gfloat4p L = leaves + (kLeafFloats / 4) * (size_t)li;
+      const uint32_t count = (id >> 27) & 0xFu, first = id & ((1u << 27) - 1u);
+      const gfloat4p L = leaves + 3 * (size_t)first;
       if (STATS) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
       for (uint32_t i = 0; i < count; ++i) {  // the running t_max: the first of equal hits stays
         double t, u, v;
@@ -763,7 +763,7 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
         if (leaf_tri_hit(ld4(L, 3 * i), ld4(L, 3 * i + 1), p2, ro, rd, tmin, tmax, t, u, v)) {
           tmax = t;
           t_hit = t; u_hit = u; v_hit = v;
-          tri = __float_as_uint(p2.y);
+          tri = first + i;
           found = true;
         }
       }
@@ -995,11 +995,11 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
       bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
-        const uint32_t count = (node >> 27) & 0xFu, li = node & ((1u << 27) - 1u);
+        const uint32_t count = (node >> 27) & 0xFu, first = node & ((1u << 27) - 1u);
         double t = INFINITY, u = 0.0, v = 0.0;
-        uint32_t key = 4u, id = 0u;
+        uint32_t key = 4u, id = 0u, li = 0u;
         if (c < count) {
-          const gfloat4p R = leaves + (kLeafFloats / 4) * (size_t)li + 3 * c;
+          const gfloat4p R = leaves + 3 * (size_t)(first + c);
           float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
           // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
           asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
@@ -1008,9 +1008,11 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
           // back: the tie goes to the reference's visiting order below)
           if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tin, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
-            t = tt; u = uu; v = vv; key = c; id = __float_as_uint(p2.y);
+            t = tt; u = uu; v = vv; key = c; id = first + c;
           }
+          li = __float_as_uint(p2.y);
         }
+        li = quad_perm<0x00>(li);  // the leaf's index, from lane 0's record (count >= 1)
         if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
         quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
         quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
@@ -1127,7 +1129,16 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
 __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double t, uint32_t tri, double u, double v, Hit& h) {
   const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
   const double w = 1.0 - u - v;
-  const double* nn = M.normals + 9 * (size_t)tri;
+  double nn[9];
+  if (M.normals32) {  // exact f32 values (OBJ vn)
+    const float* f = M.normals32 + 9 * (size_t)tri;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) nn[k] = (double)f[k];
+  } else {
+    const double* f = M.normals + 9 * (size_t)tri;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) nn[k] = f[k];
+  }
   const double onx = nn[0] * w + nn[3] * u + nn[6] * v;
   const double ony = nn[1] * w + nn[4] * u + nn[7] * v;
   const double onz = nn[2] * w + nn[5] * u + nn[8] * v;
