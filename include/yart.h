@@ -210,6 +210,11 @@ typedef struct yart_scene_info {
   uint64_t device_bytes;  /* HBM held by the scene                                      */
   uint32_t world_nodes;   /* world BVH nodes over the object list (0 = linear walk)     */
   uint32_t world_depth;   /* its deepest root-to-leaf path                              */
+  uint32_t bvh_tied_cuts; /* QBVH median cuts inside a run of equal centroid keys:
+                             where Rust's unstable sort (qbvh.rs:679-685) may order differently */
+  uint32_t bvh_tied_leaves; /* leaves whose triangle order rests on equal keys              */
+  double bvh_build_ms;    /* host QBVH build time, all meshes                           */
+  double upload_ms;       /* host -> device copies of the scene                         */
 } yart_scene_info;
 
 /* Per-launch work counters (optional, for roofline accounting; they slow the kernel). */
@@ -338,6 +343,22 @@ int yart_finalize_rgba8(int device, const double* xyz_sum, uint32_t width, uint3
  * world object hit or -1 (then hits[] is left as NaN). Host buffers. */
 int yart_intersect(yart_scene* scene, const double* rays, uint32_t n, double* hits,
                    int32_t* obj);
+
+/* Host-only QBVH build (no device): the L4QBVH of scene creation for one mesh, reported
+ * without uploading it — build time, shape, the tie exposure and a digest of the device
+ * arrays (FNV-1a 64 over node records, triangle records, leaf records, normals), so builder
+ * variants can be compared byte for byte. flags: YART_QBVH_TIES_DESC orders equal centroid
+ * keys by descending input index instead of ascending (the probe of sort_unstable_by's freedom,
+ * qbvh.rs:679-685); YART_QBVH_SERIAL builds on one thread. */
+#define YART_QBVH_TIES_DESC 1u
+#define YART_QBVH_SERIAL 2u
+typedef struct yart_qbvh_build_info {
+  uint32_t nodes, leaves, depth, tied_cuts, tied_leaves, reserved;
+  uint64_t digest;
+  double build_ms;
+} yart_qbvh_build_info;
+int yart_qbvh_build(const float* positions, const double* normals, uint32_t n_triangles, uint32_t flags,
+                    yart_qbvh_build_info* out);
 
 /* Test probes (device side of the parity tests). */
 /* The per-sample random stream: n draws of gen::<f64>() for (pixel, sample). */

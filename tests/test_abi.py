@@ -63,6 +63,7 @@ int main(void) {
          sizeof(yart_render_params), sizeof(yart_scene_info), sizeof(yart_render_stats), sizeof(yart_render_defaults),
          sizeof(yart_cli), sizeof(yart_render_options));
   printf("%zu %zu %zu\n", offsetof(yart_object, p), offsetof(yart_scene_desc, background), offsetof(yart_cli, seed));
+  printf("%zu %zu\n", sizeof(yart_qbvh_build_info), offsetof(yart_scene_info, bvh_build_ms));
   return 0;
 }
 ''')
@@ -73,6 +74,7 @@ int main(void) {
             abi.SceneInfo, abi.RenderStats, abi.RenderDefaults, abi.Cli, abi.RenderOptions]
     assert [int(x) for x in got[0].split()] == [C.sizeof(t) for t in want]
     assert [int(x) for x in got[1].split()] == [abi.Object.p.offset, abi.SceneDesc.background.offset, abi.Cli.seed.offset]
+    assert [int(x) for x in got[2].split()] == [C.sizeof(abi.QbvhBuildInfo), abi.SceneInfo.bvh_build_ms.offset]
 
 
 def test_shard_packed_len_is_the_packed_layout():

@@ -1,0 +1,52 @@
+"""The host QBVH builder (L4QBVH::new, qbvh.rs:252-361) without a GPU: the threaded build is
+byte-identical to the sequential one, the reference's shape for the repo's meshes, and the
+exposure to Rust's sort_unstable_by tie freedom (qbvh.rs:679-685) counted and pinned."""
+import pytest
+
+import yart
+
+MESHES = {  # name: (triangles, inner nodes, leaves, depth)
+    "cube": (12, 1, 4, 1),
+    "david": (46664, 5461, 16384, 7),
+    "sycee": (31642, 5461, 16384, 7),
+}
+
+
+@pytest.fixture(scope="module")
+def meshes(repo):
+    return {n: yart.load_obj(repo / "assets" / f"{n}.obj") for n in MESHES}
+
+
+@pytest.mark.parametrize("name", list(MESHES))
+def test_threaded_build_is_byte_identical_to_sequential(meshes, name):
+    pos, nrm = meshes[name]
+    par = yart.qbvh_build(pos, nrm)
+    seq = yart.qbvh_build(pos, nrm, yart.QBVH_SERIAL)
+    assert par["digest"] == seq["digest"]
+    n_tris, nodes, leaves, depth = MESHES[name]
+    assert len(pos) == n_tris
+    assert (par["nodes"], par["leaves"], par["depth"]) == (nodes, leaves, depth)
+    assert par["build_ms"] > 0.0
+
+
+# Cuts that fall inside a run of equal centroid keys, and leaves whose lane order rests on equal
+# keys: where the reference's unstable sort may order the tree differently from this build's
+# input-index rule. The counts agree with an independent replay of the split.
+@pytest.mark.parametrize("name,cuts,leaves", [("david", 3943, 6709), ("sycee", 4978, 4466)])
+def test_tie_exposure_is_counted(meshes, name, cuts, leaves):
+    pos, nrm = meshes[name]
+    info = yart.qbvh_build(pos, nrm)
+    assert (info["tied_cuts"], info["tied_leaves"]) == (cuts, leaves)
+    flipped = yart.qbvh_build(pos, nrm, yart.QBVH_TIES_DESC)
+    # the opposite tie order builds a different tree of the same shape (the GPU test
+    # test_qbvh_tie_order_does_not_change_hits renders and intersects with both)
+    assert flipped["digest"] != info["digest"]
+    assert (flipped["nodes"], flipped["leaves"], flipped["depth"]) == (info["nodes"], info["leaves"], info["depth"])
+
+
+def test_degenerate_meshes_are_refused(meshes):
+    pos, nrm = meshes["cube"]
+    with pytest.raises(yart.YartError):
+        yart.qbvh_build(pos[:4], nrm[:4])
+    yart.qbvh_build(pos, nrm)  # a successful call clears yart_last_error (thread-local)
+    assert yart.load_device().yart_last_error().decode() == ""

@@ -55,10 +55,13 @@ def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False)
                           "node_visits": c.node_visits, "leaf_visits": c.leaf_visits, "leaf_tris": c.leaf_tris,
                           "light_tests": c.light_tests, "mesh_rewalks": c.mesh_rewalks, "coop_rounds": c.coop_rounds, "coop_leaf_rounds": c.coop_leaf_rounds, "coop_walks": c.coop_walks}
         info = s.info()
+        line["scene_build_ms"] = round(info.bvh_build_ms, 2)   # host QBVH build (threaded), all meshes
+        line["scene_upload_ms"] = round(info.upload_ms, 2)     # host -> device copies
         if info.bvh_nodes:
+            line["bvh_tied_cuts"] = info.bvh_tied_cuts
             # algorithmic bytes of the traversal: 128 B per inner node visit,
-            # 144 B per leaf block, 72 B of normals per accepted hit ~ segment
-            b = 128 * c.node_visits + 144 * c.leaf_visits + 72 * c.segments
+            # 48 B per tested triangle record, at most 72 B of normals per segment
+            b = 128 * c.node_visits + 48 * c.leaf_tris + 72 * c.segments
             line["traversal_bytes"] = b
             line["traversal_GBps"] = round(b / (ms * 1e-3) / 1e9, 1)
     if cpu:

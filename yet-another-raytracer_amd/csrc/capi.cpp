@@ -205,12 +205,19 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   double bg[kBins];
   for (int b = 0; b < kBins; ++b) bg[b] = spectrum_bin(d->background, b);
   std::vector<BuiltMesh> built(d->n_meshes);
-  uint32_t nodes = 0, leaves = 0, depth = 0;
+  uint32_t nodes = 0, leaves = 0, depth = 0, tied_cuts = 0, tied_leaves = 0;
+  double build_ms = 0.0;
+  QbvhOptions qopt;  // YART_QBVH_TIES=desc: the tie-order probe (tests); YART_QBVH_THREADS=n
+  if (const char* e = std::getenv("YART_QBVH_TIES")) qopt.ties_desc = std::strcmp(e, "desc") == 0;
+  if (const char* e = std::getenv("YART_QBVH_THREADS")) qopt.threads = (uint32_t)std::max(0, std::atoi(e));
   for (uint32_t m = 0; m < d->n_meshes; ++m) {
     const yart_mesh& ym = d->meshes[m];
     if (!ym.positions || !ym.normals) return fail(YART_ERR_INVALID, "mesh without positions/normals");
     std::string err;
-    if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err)) return fail(YART_ERR_UNSUPPORTED, err);
+    if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err, qopt)) return fail(YART_ERR_UNSUPPORTED, err);
+    tied_cuts += built[m].tied_cuts;
+    tied_leaves += built[m].tied_leaves;
+    build_ms += built[m].build_ms;
     nodes += (uint32_t)built[m].nodes.size();
     leaves += (uint32_t)built[m].aux.size();
     depth = std::max(depth, built[m].depth);
@@ -236,6 +243,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     s->cu_count = 256;
   uint64_t bytes = 0;
   DevScene& ds = s->dev;
+  const auto up0 = std::chrono::steady_clock::now();
   HIP_TRY(upload(s->owned, objs.data(), objs.size(), &ds.objects, bytes), "upload objects");
   HIP_TRY(upload(s->owned, lights.data(), lights.size(), &ds.lights, bytes), "upload lights");
   HIP_TRY(upload(s->owned, mats.data(), mats.size(), &ds.materials, bytes), "upload materials");
@@ -298,11 +306,43 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   in.device_bytes = bytes;
   in.world_nodes = use_world ? (uint32_t)world.nodes.size() : 0;
   in.world_depth = use_world ? world.depth : 0;
+  in.bvh_tied_cuts = tied_cuts;
+  in.bvh_tied_leaves = tied_leaves;
+  in.bvh_build_ms = build_ms;
+  in.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - up0).count();
   *out = s.release();
   return ok();
 }
 
 void yart_scene_destroy(yart_scene* s) { delete s; }
+
+int yart_qbvh_build(const float* positions, const double* normals, uint32_t n, uint32_t flags, yart_qbvh_build_info* out) {
+  if (!positions || !normals || !out) return fail(YART_ERR_INVALID, "null argument");
+  BuiltMesh b;
+  std::string err;
+  QbvhOptions opt;
+  opt.ties_desc = (flags & YART_QBVH_TIES_DESC) != 0;
+  opt.threads = (flags & YART_QBVH_SERIAL) ? 1u : 0u;
+  if (!build_qbvh(n, positions, normals, b, err, opt)) return fail(YART_ERR_UNSUPPORTED, err);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+  auto mix = [&h](const void* p, size_t len) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < len; ++i) { h ^= c[i]; h *= 1099511628211ull; }
+  };
+  mix(b.nodes.data(), b.nodes.size() * sizeof(DevNode));
+  mix(b.leaves.data(), b.leaves.size() * sizeof(float));
+  mix(b.aux.data(), b.aux.size() * sizeof(LeafAux));
+  mix(b.normals.data(), b.normals.size() * sizeof(double));
+  std::memset(out, 0, sizeof *out);
+  out->nodes = (uint32_t)b.nodes.size();
+  out->leaves = (uint32_t)b.aux.size();
+  out->depth = b.depth;
+  out->tied_cuts = b.tied_cuts;
+  out->tied_leaves = b.tied_leaves;
+  out->digest = h;
+  out->build_ms = b.build_ms;
+  return ok();
+}
 
 int yart_scene_get_info(const yart_scene* s, yart_scene_info* out) {
   if (!s || !out) return fail(YART_ERR_INVALID, "null argument");

@@ -103,6 +103,7 @@ def load_device():
     _sig(L, "yart_render_multi", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, abi.PROGRESS_FN, P)
     _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
     _sig(L, "yart_multi_destroy", None, P)
+    _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
     _dev = L
     return L
 
@@ -233,6 +234,31 @@ class DeviceScene:
         obj = np.empty(n, dtype=np.int32)
         _check_dev(load_device().yart_intersect(self._s, _ptr(rays), n, _ptr(hits), _ptr(obj)))
         return hits, obj
+
+
+QBVH_TIES_DESC, QBVH_SERIAL = 1, 2
+
+
+def load_obj(path):
+    """TriangleMesh::from_obj's triangles (tobj semantics, libyart_host): f32 positions (n, 9) and
+    f64 normals (n, 9)."""
+    H = load_host()
+    n = C.c_uint32()
+    _check_host(H.yart_obj_triangle_count(str(path).encode(), C.byref(n)))
+    pos = np.zeros((n.value, 9), np.float32)
+    nrm = np.zeros((n.value, 9), np.float64)
+    uv = np.zeros((n.value, 6), np.float64)
+    _check_host(H.yart_obj_load(str(path).encode(), _ptr(pos), _ptr(nrm), _ptr(uv), n.value))
+    return pos, nrm
+
+
+def qbvh_build(positions, normals, flags=0):
+    """Host-only L4QBVH build (yart_qbvh_build): shape, tie exposure, digest and build time."""
+    positions = np.ascontiguousarray(positions, np.float32)
+    normals = np.ascontiguousarray(normals, np.float64)
+    info = abi.QbvhBuildInfo()
+    _check_dev(load_device().yart_qbvh_build(_ptr(positions), _ptr(normals), len(positions), flags, C.byref(info)))
+    return {k: getattr(info, k) for k, _ in info._fields_ if k != "reserved"}
 
 
 def finalize_rgba8(xyz_sum, spp, device=0):

@@ -68,7 +68,14 @@ class SceneInfo(C.Structure):
     _fields_ = [("device", C.c_int), ("n_objects", C.c_uint32), ("n_lights", C.c_uint32), ("n_meshes", C.c_uint32),
                 ("bvh_nodes", C.c_uint32), ("bvh_leaves", C.c_uint32), ("bvh_max_depth", C.c_uint32),
                 ("bvh_max_stack", C.c_uint32), ("device_bytes", C.c_uint64), ("world_nodes", C.c_uint32),
-                ("world_depth", C.c_uint32)]
+                ("world_depth", C.c_uint32), ("bvh_tied_cuts", C.c_uint32), ("bvh_tied_leaves", C.c_uint32),
+                ("bvh_build_ms", C.c_double), ("upload_ms", C.c_double)]
+
+
+class QbvhBuildInfo(C.Structure):
+    _fields_ = [("nodes", C.c_uint32), ("leaves", C.c_uint32), ("depth", C.c_uint32), ("tied_cuts", C.c_uint32),
+                ("tied_leaves", C.c_uint32), ("reserved", C.c_uint32), ("digest", C.c_uint64),
+                ("build_ms", C.c_double)]
 
 
 class RenderStats(C.Structure):
@@ -107,7 +114,7 @@ DEVICE_SYMBOLS = [
     "yart_finalize_rgba8_async", "yart_finalize_rgba8", "yart_intersect", "yart_probe_rng", "yart_probe_math",
     "yart_shard_packed_len", "yart_render_packed_async", "yart_comm_unique_id", "yart_comm_init_rank",
     "yart_comm_init_all", "yart_comm_destroy", "yart_gather_frame_async", "yart_multi_create", "yart_render_multi",
-    "yart_multi_last_timing", "yart_multi_destroy",
+    "yart_multi_last_timing", "yart_multi_destroy", "yart_qbvh_build",
 ]
 COMM_ID_BYTES = 128
 HOST_SYMBOLS = [
