@@ -1576,11 +1576,11 @@ __device__ __forceinline__ uint32_t sat_u32(double f) {
   return (uint32_t)f;
 }
 
+// `bin` = spectrum_bin(λ) of the path's wavelength (fixed along a path: computed once per sample).
 template <bool EXT>
-__device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, double wl, V3 p, double hu = 0.0,
+__device__ __forceinline__ double texture_value(const DevScene& S, uint32_t ti, int bin, V3 p, double hu = 0.0,
                                                 double hv = 0.0) {
   const DevTexture& t = S.textures[ti];
-  const int bin = spectrum_bin(wl);
   if (EXT && t.kind == YART_TEX_IMAGE) {  // ImageTexture::value texture.rs:320-344
     if (!t.pixels || t.width == 0 || t.height == 0) return 1.0;
     const double uu = clampd(hu, 0.0, 1.0), vv = 1.0 - clampd(hv, 0.0, 1.0);
@@ -1746,6 +1746,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   V3 hp = mk(0.0, 0.0, 0.0), hn = hp;  // the hit to scatter at the top of the next iteration
   uint32_t hmat = 0;
   double hu = 0.0, hv = 0.0;            // its texture coordinates (EXT)
+  int wbin = 0;                         // spectrum bin of the path's wavelength
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
 
   // The loop exits wave-uniformly: a lane without work stays in it with `run` false, so the
@@ -1816,8 +1817,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
 #ifndef YART_NO_LAUNDER
         ray = camera_ray(*kernarg_camera(), u, v, wl, g, EXT && S.has_time);
+        wbin = spectrum_bin(wl);  // the path's reflectance bin (color.rs:276-283), once per sample
 #else
         ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
+        wbin = spectrum_bin(wl);
 #endif
         T = 1.0;
         depth = A.max_depth;
@@ -1831,7 +1834,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           const uint32_t kind = m.kind;
           if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
             OCC(OCC_LAMB);
-            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
             const Onb uvw = onb_from_w(hn, mp);
             V3 dir;
             double pdf_val;
@@ -1866,7 +1869,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
               depth_ = depth - 1;
             }
           } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
             V3 p;
             for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
               const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
@@ -1886,7 +1889,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
               p = mk(px, py, pz);
               if (!(len2(p) >= 1.0)) break;
             }
-            const double att = texture_value<EXT>(S, m.texture, ray.wl, hp, hu, hv);
+            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
             T_ = T * att;
             o_ = hp;
             d_ = add(reflected, smul(m.fuzz, p));
@@ -1960,8 +1963,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       if (want) {
         if (STATS) st.v[ST_SEGMENTS]++;
         if (!hit) {
-          const int bin = spectrum_bin(ray.wl);  // background_color.reflect (main.rs:587)
-          R = T * S.background[bin];
+          R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
           term = true;
         } else {
           const DevMaterial& m = S.materials[h.mat];
@@ -1972,7 +1974,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
             if (EXT) { hu = h.u; hv = h.v; }
           } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
             double emitted = 0.0;
-            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, ray.wl, h.p, h.u, h.v);
+            if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, wbin, h.p, h.u, h.v);
             R = T * emitted;
             term = true;
           }
