@@ -266,7 +266,12 @@ def main():
                                "light_tests": st.light_tests, "node_visits": st.node_visits,
                                "leaf_tris": st.leaf_tris},
                     "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None),
-                    "valu_issue_busy": valu_issue(pmc) if world == 1 else None}
+                    # the sample scratch k_render writes (24 B of XYZ per sample)
+                    "algorithmic_bytes_per_launch": st.samples * 24 if accum_ms > 0 else None,
+                    "valu_issue_busy": valu_issue(pmc) if world == 1 else None,
+                    # wave-level VALU instructions (SQ_INSTS_VALU of the snapshot) per path segment
+                    "valu_insts_per_segment": (round(pmc["SQ_INSTS_VALU"] / st.segments, 2)
+                                               if world == 1 and pmc.get("SQ_INSTS_VALU") and st.segments else None)}
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
 
