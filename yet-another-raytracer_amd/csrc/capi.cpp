@@ -110,7 +110,39 @@ DevObject to_dev(const yart_object& o) {
     }
   }
   for (int k = 0; k < 24; ++k) d.p[k] = o.p[k];
+  d.lpf = kNoLpf;
   return d;
+}
+
+// Light-pdf capture slots (device_types.h): every light whose pdf_value intersects (no wrapper,
+// XZRect or StillSphere: hittable.rs:28-30 gives the others 0) is paired with a world object that
+// is the same primitive — same kind and parameters, no wrapper but FlipFace (which leaves the ray
+// and t alone) — so the world pass of the sampled ray yields exactly the t and hit pdf_value
+// computes. All or nothing: a light without a partner, or more than kMaxLpf of them, leaves the
+// scene on the reference's re-intersection. YART_LPF=0 forces that (A/B).
+uint32_t assign_lpf(std::vector<DevObject>& objs, std::vector<DevObject>& lights) {
+  if (const char* e = std::getenv("YART_LPF"))
+    if (std::atoi(e) == 0) return 0;
+  uint32_t n = 0;
+  for (DevObject& l : lights) {
+    if (l.n_xf != 0 || (l.kind != YART_PRIM_XZ_RECT && l.kind != YART_PRIM_SPHERE)) continue;
+    const int np = l.kind == YART_PRIM_SPHERE ? 4 : 5;
+    DevObject* partner = nullptr;
+    for (DevObject& o : objs) {
+      if (o.kind != l.kind || o.lpf != kNoLpf) continue;
+      bool same = true, plain = o.n_xf <= (uint32_t)kMaxXforms;
+      for (int k = 0; k < np; ++k) same &= std::memcmp(&o.p[k], &l.p[k], sizeof(double)) == 0;
+      for (uint32_t w = 0; w < o.n_xf && w < (uint32_t)kMaxXforms; ++w) plain &= o.xf_kind[w] == YART_XF_FLIP_FACE;
+      if (same && plain) { partner = &o; break; }
+    }
+    if (!partner || n == kMaxLpf) {
+      for (DevObject& o : objs) o.lpf = kNoLpf;
+      for (DevObject& x : lights) x.lpf = kNoLpf;
+      return 0;
+    }
+    partner->lpf = l.lpf = n++;
+  }
+  return n;
 }
 
 }  // namespace
@@ -236,6 +268,13 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     if (want && !any_mesh) use_world = build_world_bvh(objs, world);
   }
 
+  uint32_t n_lpf = 0;
+  {
+    bool any_mesh = false;
+    for (uint32_t i = 0; i < d->n_objects; ++i) any_mesh |= d->objects[i].kind == YART_PRIM_MESH;
+    if (!use_world && !any_mesh) n_lpf = assign_lpf(objs, lights);  // the list kernels capture
+  }
+
   auto s = std::make_unique<yart_scene>();
   s->device = device;
   DeviceGuard guard(device);
@@ -288,6 +327,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
+  ds.n_lpf = n_lpf;
   ds.has_mesh = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
   ds.has_ext = 0;

@@ -499,6 +499,25 @@ __device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double t
   }
   return true;
 }
+// sphere_t that also reports whether a root lies in [t_min, inf) (pdf_value's test, sphere.rs:96).
+// Both roots are computed; the finite-t_max answer follows sphere_t's own steps.
+__device__ __forceinline__ bool sphere_t_cap(const double* p, const Ray& r, double tmin, double tmax, double& t, bool& hit_inf) {
+  V3 center = mk(p[0], p[1], p[2]);
+  double radius = p[3];
+  V3 oc = sub(r.o, center);
+  double a = len2(r.d);
+  double half_b = dot(oc, r.d);
+  double c = len2(oc) - radius * radius;
+  double disc = half_b * half_b - a * c;
+  hit_inf = false;
+  if (disc < 0.0) return false;
+  double sq = sqrt(disc);
+  const double t1 = (0.0 - half_b - sq) / a, t2 = (0.0 - half_b + sq) / a;
+  hit_inf = !(t1 < tmin) || !(t2 < tmin);  // inf < t never holds
+  if (!(t1 < tmin || tmax < t1)) { t = t1; return true; }
+  if (!(t2 < tmin || tmax < t2)) { t = t2; return true; }
+  return false;
+}
 template <bool UV = false, class M = Ieee>
 __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h, M&& m = M()) {
   V3 center = mk(p[0], p[1], p[2]);
@@ -573,6 +592,19 @@ __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmi
   double y = o[CC] + t * d[CC];
   if (x < p[0] || x > p[1] || y < p[2] || y > p[3]) return false;
   return true;
+}
+// rect_t that also reports the test over [t_min, inf) — the one pdf_value makes (aarect.rs:149):
+// the same t, and the bounds checked whatever t_max says. Returns rect_t's answer.
+template <int A, int B, int CC>
+__device__ __forceinline__ bool rect_t_cap(const double* p, const Ray& r, double tmin, double tmax, double& t, bool& hit_inf) {
+  const double* o = &r.o.x;
+  const double* d = &r.d.x;
+  const double num = p[4] - o[A], den = d[A];
+  t = num / den;
+  const double x = o[B] + t * d[B];
+  const double y = o[CC] + t * d[CC];
+  hit_inf = !(t < tmin) && !(x < p[0] || x > p[1] || y < p[2] || y > p[3]);  // t > inf never holds
+  return hit_inf && !(t > tmax);
 }
 // Record of an axis-aligned rect with plane axis `a` (0 yz, 1 xz, 2 xy); a runtime axis lets the
 // rect and box-face records of a wave share one code path.
@@ -1153,6 +1185,10 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 // ------------------------------------------------------------------------ world hit
 // Which primitive of the world list won, and where: enough to rebuild its record exactly.
 struct HitId { double t, u, v; uint32_t obj, sub; };
+// What the world pass captured for the light-pdf slots (device_types.h kMaxLpf).
+// The t's go to LDS (the lane's column of a [slot][lane] array): held in registers across the
+// world pass they pushed the list kernel into spilling inside its object loop (-12 %).
+struct LightCap { double* t; bool hit[kMaxLpf]; };
 
 template <bool HAS_MESH, bool STATS>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
@@ -1225,9 +1261,12 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // dead-but-compiled code: registers and spills).
 // HAS_MESH: called from converged code by all 64 lanes, `want` marking the lanes with a query —
 // meshes are walked cooperatively (qbvh_coop) by the whole wave, the other objects per lane.
-template <bool HAS_MESH, bool STATS, bool EXT>
+// LPF: objects holding a light-pdf slot are tested with the capture forms (rect_t_cap /
+// sphere_t_cap: the same t and answer as prim_t, plus the [t_min, inf) test pdf_value makes).
+template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
-                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
+                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
+                                              LightCap* cap = nullptr) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -1250,8 +1289,24 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       const Ray lr = to_local(o, nxf, r);
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
-      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+      bool hit = false;
+      if (LPF && o.lpf < kMaxLpf) {  // wave-uniform; no wrapper but FlipFace: lr is r
+        if (STATS) st.v[ST_PRIM]++;
+#pragma unroll
+        for (uint32_t k = 0; k < kMaxLpf; ++k) {
+          if (o.lpf == k) {
+            if (kind == YART_PRIM_SPHERE) {
+              hit = sphere_t_cap(o.p, lr, tmin, closest, t, cap->hit[k]);
+            } else {
+              hit = rect_t_cap<1, 0, 2>(o.p, lr, tmin, closest, t, cap->hit[k]);
+              cap->t[k * 64] = t;
+            }
+          }
+        }
+      } else {
+        hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                     : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+      }
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1405,14 +1460,15 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS, bool EXT>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
+                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
+                                          LightCap* cap = nullptr) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT>(S, want, r, tmin, tmax, id, stk, coop, st, q) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, LPF>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -1447,28 +1503,40 @@ __device__ __forceinline__ double cosine_value(const Onb& b, V3 d, M& m) {  // p
   return cosine <= 0.0 ? 0.0 : cosine / kPi;
 }
 
-template <bool STATS, class M>
-__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st, M& m) {
-  if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
-  Ray r{origin, dir, 0.0, wl};
-  Hit h;
+// pdf_value of a light that was hit (or not) at t over [0.001, inf) by (origin, dir).
+template <class M>
+__device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3 dir, bool hit, double t, M& m) {
+  if (!hit) return 0.0;
   if (o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:148-162
-    if (STATS) st.v[ST_LIGHT]++;
-    if (!xz_hit(o.p, r, 0.001, INFINITY, h)) return 0.0;
+    Hit h;
+    rect_rec(1, Ray{origin, dir, 0.0, 0.0}, t, h);
     const double area = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
     const double distance_squared = h.t * h.t * len2(dir);
     const double cosine = fabs(dot(dir, h.n)) / m.len(dir);
     return distance_squared / (cosine * area);
   }
-  if (o.kind == YART_PRIM_SPHERE) {  // sphere.rs:95-110
+  // sphere.rs:95-110
+  const double radius = o.p[3];
+  const double cos_theta_max = m.sqrt(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
+  const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
+  return 1.0 / solid_angle;
+}
+template <bool STATS, class M>
+__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st, M& m) {
+  if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
+  Ray r{origin, dir, 0.0, wl};
+  double t = 0.0;
+  bool hit;
+  if (o.kind == YART_PRIM_XZ_RECT) {
     if (STATS) st.v[ST_LIGHT]++;
-    if (!sphere_hit(o.p, r, 0.001, INFINITY, h, m)) return 0.0;
-    const double radius = o.p[3];
-    const double cos_theta_max = m.sqrt(1.0 - radius * radius / len2(sub(ld3(o.p), origin)));
-    const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
-    return 1.0 / solid_angle;
+    hit = rect_t<1, 0, 2>(o.p, r, 0.001, INFINITY, t);
+  } else if (o.kind == YART_PRIM_SPHERE) {
+    if (STATS) st.v[ST_LIGHT]++;
+    hit = sphere_t(o.p, r, 0.001, INFINITY, t, m);
+  } else {
+    return 0.0;
   }
-  return 0.0;
+  return light_pdf_at(o, origin, dir, hit, t, m);
 }
 template <class M>
 __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g, M& m) {
@@ -1701,9 +1769,17 @@ __device__ unsigned long long g_occ[32];
 #define OCC(k) do {} while (0)
 #endif
 
+#ifndef YART_LPF
+#define YART_LPF 0
+#endif
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
 __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[HAS_MESH ? 4 * kWaveLdsWords : BVH ? 4 * kStackSlots * 64 : 1];
+  // LPF (build with -DYART_LPF=1): the list kernels capture light hits in the world pass. Off by
+  // default — bitwise either way, but measured slower: cornell 4,174 vs 4,585 Msamples/s (the extra
+  // code in the object loop and the deferred state cost more registers than the re-tests it saves).
+  constexpr bool LPF = YART_LPF && !HAS_MESH && !BVH;
+  __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
   // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
@@ -1720,6 +1796,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
+  double* const lpf_lds = &s_lpf[LPF ? wave * 256 + lane : 0];
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
   Stats st;
@@ -1802,6 +1879,40 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     if (__ballot(run) == 0) break;
     double R = 0.0;
     bool term = false, want = false;
+    // LPF: a Lambertian scatter's mixture pdf waits for the world pass of the ray it sampled,
+    // which captures the light hits pdf_value would re-test (device_types.h kMaxLpf): T·att·spdf
+    // (Tp) and the cosine half (cosv) are kept until then, T stays the incoming throughput.
+    bool pend = false;
+    double* const Tp = &lpf_lds[0], * const cosv = &lpf_lds[64];  // LDS, [value][lane]
+    // Every light whose pdf_value intersects holds a slot (capi.cpp assign_lpf: all or none); the
+    // others' pdf_value is 0 (hittable.rs:28-30).
+    auto resolve = [&](const LightCap& c) {  // hittable.rs:103-111 + pdf.rs mixture, material.rs:56-60
+      Ieee im;
+      const double weight = 1.0 / (double)S.n_lights;
+      double sum = -0.0;
+      for (uint32_t i = 0; i < S.n_lights; ++i) {
+        const DevObject& L = S.lights[i];
+        double v = 0.0;
+        if (L.lpf < kMaxLpf) {  // wave-uniform
+          if (STATS) st.v[ST_LIGHT]++;
+          bool h = false;
+          double t = 0.0;
+#pragma unroll
+          for (uint32_t k = 0; k < kMaxLpf; ++k)
+            if (L.lpf == k) { h = c.hit[k]; t = c.t[k * 64]; }
+          v = light_pdf_at(L, ray.o, ray.d, h, t, im);
+        }
+        sum = sum + weight * v;
+      }
+      const double pdf_val = 0.5 * sum + 0.5 * *cosv;
+      pend = false;
+      if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+        R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+        term = true;
+      } else {
+        T = *Tp / pdf_val;
+      }
+    };
     if (run) {
       OCC(OCC_ITER);
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
@@ -1828,8 +1939,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
-        auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_) {
-          T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false;
+        auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
+                           double& Tp_, double& cosv_, bool& pend_) {
+          T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false; pend_ = false;
           const DevMaterial& m = S.materials[hmat];
           const uint32_t kind = m.kind;
           if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
@@ -1852,12 +1964,25 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
                 OCC(OCC_LAMB_COS);
                 dir = local(uvw, random_cosine_direction(g, mp));
               }
-              const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-              double sum = -0.0;
-              for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
-              pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
+              if (LPF && S.n_lpf != 0) {  // finished after the world pass (resolve)
+                pdf_val = 0.0;
+                cosv_ = cosine_value(uvw, dir, mp);
+                pend_ = true;
+              } else {
+                const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+                double sum = -0.0;
+                for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
+                pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
+              }
             }
-            if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+            if (pend_) {
+              const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+              const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+              Tp_ = (T * att) * spdf;
+              o_ = hp;
+              d_ = dir;
+              depth_ = depth - 1;
+            } else if (!isfinite(pdf_val) || pdf_val <= 0.0) {
               R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
               term_ = true;
             } else {
@@ -1927,24 +2052,26 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
             depth_ = depth - 1;
           }
         };
-        double nT, nR;
+        double nT, nR, nTp = 0.0, ncosv = 0.0;
         V3 no, nd;
         uint32_t ndepth;
-        bool nterm;
+        bool nterm, npend;
         FastMath fm;
-        scatter(fm, nT, no, nd, ndepth, nR, nterm);
+        scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
           rng_phase<!HAS_MESH && !BVH>(g, pixel, smp, A.max_depth - depth + 1u);
           Ieee im;
-          scatter(im, nT, no, nd, ndepth, nR, nterm);
+          scatter(im, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         }
         T = nT; ray.o = no; ray.d = nd; depth = ndepth; R = nR; term = nterm;
+        pend = npend;
+        if (LPF && pend) { *Tp = nTp; *cosv = ncosv; }
       }
       if (!term) {
-        if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
+        if (depth == 0 && !(LPF && pend)) {  // main.rs:544-546: exhausted depth reflects 1.0
           R = T * 1.0;
           term = true;
-        } else {
+        } else {  // (a pending pdf at depth 0 is finished by the world pass's capture, below)
           want = true;
         }
       }
@@ -1953,14 +2080,23 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       Hit h;
       int32_t which;
       bool hit = false;
+      LightCap cap;
+      cap.t = &lpf_lds[128];
       const QueryCtx q{g.k0, g.k1, smp, pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       } else if (want) {
         OCC(OCC_WALK);
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT, LPF>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q, &cap);
       }
-      if (want) {
+      if (LPF && want && pend) {
+        resolve(cap);
+        if (!term && depth == 0) {  // the sampled ray was traced only for its light hits
+          R = T * 1.0;
+          term = true;
+        }
+      }
+      if (want && !term) {
         if (STATS) st.v[ST_SEGMENTS]++;
         if (!hit) {
           R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
