@@ -235,3 +235,23 @@ def test_coverage_skips_row_224_of_a_225_row_image():  # main.rs:643-646
     m2 = O.coverage(1003, 16)  # W*col/8 vs col*(W/8) leaves interior columns unsampled
     assert not m2[:, 375].any() and m2[:, 374].all()
     assert O.coverage(800, 800).all()
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("cornell-box", 24, 24, 8), ("random-scene", 24, 16, 4), ("david", 16, 9, 2)])
+def test_recursive_and_iterative_integrators_agree(scene, w, h, spp):
+    """ray_reflectance as the reference writes it (main.rs:537-588: recursion, att * R' * spdf / pdf
+    on the way back) against the front-to-back loop the oracle and the kernel run
+    (T <- ((T * att) * spdf) / pdf, terminal value last). Same draws, same hits: the two differ only
+    by the association of the throughput product, a few ulps per bounce (<= 50 bounces), never
+    more. Measured: <= 3.3e-15 relative per pixel sum; 62-94 % of the sums are bit-identical."""
+    import yart
+    p = yart.Preset(scene)
+    cam, prm = p.camera(w, h), yart.render_params(w, h, spp, 50)
+    o = O.OracleScene(p.desc)
+    it = o.render(cam, prm, threads=8)
+    rec = o.render(cam, prm, threads=8, recursive=True)
+    nz = it != 0
+    assert (rec[~nz] == 0).all()
+    rel = np.abs(it - rec)[nz] / np.abs(it)[nz]
+    assert rel.max() <= 50 * 2 * 2.0 ** -52, rel.max()
+    assert (it == rec).mean() > 0.5

@@ -265,7 +265,10 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     const char* env = std::getenv("YART_WORLD_BVH");
     const int force = env ? std::atoi(env) : -1;
     const bool want = force == 1 || (force != 0 && d->n_objects >= kWorldBvhMinObjects);
-    if (want && !any_mesh) use_world = build_world_bvh(objs, world);
+    // YART_WORLD_BVH_SPLIT=median: the round-1 median-split tree (A/B); default SAH
+    const char* split = std::getenv("YART_WORLD_BVH_SPLIT");
+    const bool sah = !(split && std::strcmp(split, "median") == 0);
+    if (want && !any_mesh) use_world = build_world_bvh(objs, world, sah);
   }
 
   uint32_t n_lpf = 0;

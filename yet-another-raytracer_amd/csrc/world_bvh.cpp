@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <cstdio>
+#include <cstdlib>
 
 namespace yart_dev {
 
@@ -78,11 +80,73 @@ void set_box(DevWorldNode& n, const Item* it, size_t cnt) {
   n.mag = up(mag + pad);
 }
 
-void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, uint32_t level, BuiltWorld& out) {
+double half_area(const double lo[3], const double hi[3]) {
+  const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+  return x * y + y * z + z * x;
+}
+
+// Surface-area split of items[begin, end): the cut along one axis's centroid order that minimises
+// area(L)·|L| + area(R)·|R|, or 0 to make a leaf (at most kMaxLeaf objects, when testing them all
+// is cheaper than a node visit plus the children's expected tests). A sphere of the random scene's
+// ground (radius 1000) gets a leaf near the root this way instead of widening every box on its
+// median-split path, which every ray then visited.
+size_t kMaxLeaf = 4;
+double kNodeCost = 0.7;  // one DevWorldNode visit (two f32 box tests) vs one primitive test
+size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const double nlo[3], const double nhi[3]) {
+  const size_t n = end - begin;
+  const double parent = half_area(nlo, nhi);
+  double best = INFINITY;
+  int best_axis = -1;
+  size_t best_cut = 0;
+  std::vector<double> right(n + 1);
+  for (int axis = 0; axis < 3; ++axis) {
+    std::sort(items.begin() + begin, items.begin() + end, [axis](const Item& a, const Item& b) {
+      return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.idx < b.idx);
+    });
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = n; i-- > 1;) {  // right[i]: area of items[begin + i, end)
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], items[begin + i].lo[k]); hi[k] = std::max(hi[k], items[begin + i].hi[k]); }
+      right[i] = half_area(lo, hi);
+    }
+    for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+    for (size_t i = 1; i < n; ++i) {  // cut before items[begin + i]
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], items[begin + i - 1].lo[k]); hi[k] = std::max(hi[k], items[begin + i - 1].hi[k]); }
+      const double cost = half_area(lo, hi) * (double)i + right[i] * (double)(n - i);
+      if (cost < best) { best = cost; best_axis = axis; best_cut = i; }
+    }
+  }
+  if (best_axis < 0) return 0;
+  if (n <= kMaxLeaf && parent > 0.0 && (double)n * parent <= kNodeCost * parent + best) return 0;
+  std::sort(items.begin() + begin, items.begin() + end, [best_axis](const Item& a, const Item& b) {
+    return a.c[best_axis] < b.c[best_axis] || (a.c[best_axis] == b.c[best_axis] && a.idx < b.idx);
+  });
+  return best_cut;
+}
+
+void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, uint32_t level, BuiltWorld& out,
+           bool sah) {
   out.depth = std::max(out.depth, level);
   DevWorldNode& n = out.nodes[node];
   set_box(n, items.data() + begin, end - begin);
-  if (end - begin <= 2) {
+  size_t cut = 0;
+  // SAH near the root; median splits below level 16 bound the depth (the device walk keeps one
+  // stack slot per level, kStackSlots)
+  if (sah && level < 16 && end - begin > 1) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = begin; i < end; ++i)
+      for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], items[i].lo[k]); hi[k] = std::max(hi[k], items[i].hi[k]); }
+    cut = sah_split(items, begin, end, lo, hi);
+    if (cut == 0) {  // a leaf
+      n.count = (uint32_t)(end - begin);
+      n.first = (uint32_t)out.objs.size();
+      std::vector<uint32_t> ids;
+      for (size_t i = begin; i < end; ++i) ids.push_back(items[i].idx);
+      std::sort(ids.begin(), ids.end());
+      out.objs.insert(out.objs.end(), ids.begin(), ids.end());
+      return;
+    }
+  }
+  if (cut == 0 && end - begin <= 2) {
     n.count = (uint32_t)(end - begin);
     n.first = (uint32_t)out.objs.size();
     std::vector<uint32_t> ids;
@@ -97,22 +161,25 @@ void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, ui
   int axis = 0;
   for (int k = 1; k < 3; ++k)
     if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
-  const size_t mid = (begin + end) / 2;
-  std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end, [axis](const Item& a, const Item& b) {
-    return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.idx < b.idx);
-  });
+  size_t mid = begin + cut;
+  if (cut == 0) {
+    mid = (begin + end) / 2;
+    std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end, [axis](const Item& a, const Item& b) {
+      return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.idx < b.idx);
+    });
+  }
   const uint32_t left = (uint32_t)out.nodes.size();
   out.nodes.emplace_back();
   out.nodes.emplace_back();
   out.nodes[node].count = 0;
   out.nodes[node].first = left;
-  build(items, begin, mid, left, level + 1, out);
-  build(items, mid, end, left + 1, level + 1, out);
+  build(items, begin, mid, left, level + 1, out, sah);
+  build(items, mid, end, left + 1, level + 1, out, sah);
 }
 
 }  // namespace
 
-bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out) {
+bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah) {
   out = BuiltWorld{};
   if (objs.empty()) return false;
   std::vector<Item> items(objs.size());
@@ -121,10 +188,18 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out) {
     for (int k = 0; k < 3; ++k) items[i].c[k] = 0.5 * (items[i].lo[k] + items[i].hi[k]);
     items[i].idx = (uint32_t)i;
   }
+  // YART_WORLD_SAH=node_cost,max_leaf: tuning sweeps (tools/gpu_world.sh)
+  if (const char* e = std::getenv("YART_WORLD_SAH")) {
+    double c = 0.0;
+    unsigned l = 0;
+    if (std::sscanf(e, "%lf,%u", &c, &l) == 2 && c > 0.0 && l >= 1) { kNodeCost = c; kMaxLeaf = l; }
+  }
   out.nodes.reserve(2 * objs.size());
   out.nodes.emplace_back();
-  build(items, 0, items.size(), 0, 0, out);
-  return true;
+  build(items, 0, items.size(), 0, 0, out, sah);
+  // the device walk pushes at most one entry per level into its kStackSlots-deep stack
+  if (sah && out.depth >= (uint32_t)kStackSlots) return build_world_bvh(objs, out, false);
+  return out.depth < (uint32_t)kStackSlots;
 }
 
 }  // namespace yart_dev

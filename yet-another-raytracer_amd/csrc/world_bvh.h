@@ -20,8 +20,10 @@ struct BuiltWorld {
 // false for kinds that have no box here (meshes: those scenes keep the linear walk).
 bool world_bounds(const DevObject& o, double lo[3], double hi[3]);
 
-// Median split on the centroid's widest axis down to <= 2 objects per leaf; boxes are padded by
-// 1e-7 of their magnitude and rounded outward to f32. false if some object has no box.
-bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out);
+// Surface-area-heuristic splits (sah, the default; leaves of up to 4 objects), or median splits on
+// the centroid's widest axis down to <= 2 objects per leaf; boxes are padded by 1e-7 of their
+// magnitude and rounded outward to f32. Any tree gives the linear scan's answer (the walk keeps
+// min t, ties to the later object: kernels.hip world_closest_bvh). false if some object has no box.
+bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah = true);
 
 }  // namespace yart_dev
