@@ -768,6 +768,8 @@ __device__ __forceinline__ bool leaf_tri_hit(float4 p0, float4 p1, float4 p2, co
   const double qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
   v = f * (rd[0] * qx + rd[1] * qy + rd[2] * qz);
   t = f * (e2x * qx + e2y * qy + e2z * qz);
+  // Short-circuited on purpose: in a leaf round only the lanes of quads at a leaf test triangles,
+  // and when all of them fail an early condition the wave skips the rest (branch-free: david -4.5 %).
   return !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 && t >= tmin && tmax > t;
 }
 
@@ -1477,17 +1479,21 @@ __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ra
 
 
 // ----------------------------------------------------------------------- ONB and PDFs
-struct Onb { V3 u, v, w; };
+// u = w × v is formed where local() needs it (the same expression on the same inputs): kept as a
+// member, its three doubles were live — and spilled — through the direction sampling.
+struct Onb { V3 v, w; };
 template <class M>
 __device__ __forceinline__ Onb onb_from_w(V3 n, M& m) {  // onb.rs:10-21
   Onb b;
   b.w = m.unit(n);
   const V3 a = fabs(b.w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
   b.v = m.unit(cross(b.w, a));
-  b.u = cross(b.w, b.v);
   return b;
 }
-__device__ __forceinline__ V3 local(const Onb& b, V3 a) { return add(add(smul(a.x, b.u), smul(a.y, b.v)), smul(a.z, b.w)); }
+__device__ __forceinline__ V3 local(const Onb& b, V3 a) {
+  const V3 u = cross(b.w, b.v);
+  return add(add(smul(a.x, u), smul(a.y, b.v)), smul(a.z, b.w));
+}
 template <class M>
 __device__ __forceinline__ V3 random_cosine_direction(Rng& g, M& m) {  // pdf.rs:15-25
   const double r1 = gen_f64(g), r2 = gen_f64(g);
@@ -1772,6 +1778,9 @@ __device__ unsigned long long g_occ[32];
 #ifndef YART_LPF
 #define YART_LPF 0
 #endif
+#ifndef YART_JOBL
+#define YART_JOBL 1
+#endif
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
 __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[HAS_MESH ? 4 * kWaveLdsWords : BVH ? 4 * kStackSlots * 64 : 1];
@@ -1779,6 +1788,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // default — bitwise either way, but measured slower: cornell 4,174 vs 4,585 Msamples/s (the extra
   // code in the object loop and the deferred state cost more registers than the re-tests it saves).
   constexpr bool LPF = YART_LPF && !HAS_MESH && !BVH;
+  // JOBL (the chunked list kernels): a lane's job identity — pixel, sample, block, slot, x, y —
+  // lives in LDS ([word][lane] per wave) from its hand-out to its scratch store, read where it is
+  // used, instead of six VGPRs carried through every iteration.
+  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH && !BVH;
+  __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : 1];
   __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
@@ -1797,6 +1811,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
   double* const lpf_lds = &s_lpf[LPF ? wave * 256 + lane : 0];
+  uint32_t* const jl = &s_job[JOBL ? wave * 6 * 64 + lane : 0];
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
   Stats st;
@@ -1867,6 +1882,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           y = by0 + (slot >> 3);
           pixel = y * W + x;
           lane_blk = local_blk;
+          if (JOBL) { jl[0] = pixel; jl[64] = smp; jl[128] = lane_blk; jl[192] = slot; jl[256] = x; jl[320] = y; }
           // a pixel outside the crop grid is skipped: the lane asks again
           if ((cov >> slot) & 1ull) { fresh = true; need = false; }
         }
@@ -1918,12 +1934,12 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
-      rng_phase<!HAS_MESH && !BVH>(g, pixel, smp, fresh ? 0u : A.max_depth - depth + 1u);
+      rng_phase<!HAS_MESH && !BVH>(g, JOBL ? jl[0] : pixel, JOBL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
       if (fresh) {  // main.rs:692-698
         OCC(OCC_FRESH);
-        const double tx = (double)x + gen_f64(g);
+        const double tx = (double)(JOBL ? jl[256] : x) + gen_f64(g);
         const double u = tx / (double)(W - 1);
-        const double ty = (double)y + gen_f64(g);
+        const double ty = (double)(JOBL ? jl[320] : y) + gen_f64(g);
         const double v = 1.0 - ty / (double)(H - 1);
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
 #ifndef YART_NO_LAUNDER
@@ -1946,7 +1962,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           const uint32_t kind = m.kind;
           if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
             OCC(OCC_LAMB);
-            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
+            // the albedo is looked up where it is multiplied in: fetched here, it was held (and
+            // spilled) through the direction sampling and the light pdfs
+            auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
             const Onb uvw = onb_from_w(hn, mp);
             V3 dir;
             double pdf_val;
@@ -1978,7 +1996,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
             if (pend_) {
               const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
               const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-              Tp_ = (T * att) * spdf;
+              Tp_ = (T * att()) * spdf;
               o_ = hp;
               d_ = dir;
               depth_ = depth - 1;
@@ -1988,7 +2006,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
             } else {
               const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
               const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-              T_ = ((T * att) * spdf) / pdf_val;
+              T_ = ((T * att()) * spdf) / pdf_val;
               o_ = hp;
               d_ = dir;
               depth_ = depth - 1;
@@ -2059,7 +2077,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         FastMath fm;
         scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
-          rng_phase<!HAS_MESH && !BVH>(g, pixel, smp, A.max_depth - depth + 1u);
+          rng_phase<!HAS_MESH && !BVH>(g, JOBL ? jl[0] : pixel, JOBL ? jl[64] : smp, A.max_depth - depth + 1u);
           Ieee im;
           scatter(im, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         }
@@ -2082,7 +2100,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       bool hit = false;
       LightCap cap;
       cap.t = &lpf_lds[128];
-      const QueryCtx q{g.k0, g.k1, smp, pixel, A.max_depth - depth + 1u};
+      const QueryCtx q{g.k0, g.k1, JOBL ? jl[64] : smp, JOBL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       } else if (want) {
@@ -2130,7 +2148,8 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
       if (STATS) st.v[ST_SAMPLES]++;
       if (DYN) {  // chunked: k_accumulate adds the samples in order
-        double* q = A.scratch + 3 * (((size_t)lane_blk * A.s_count + (smp - A.s_begin)) * 64 + slot);
+        const uint32_t jb = JOBL ? jl[128] : lane_blk, js = JOBL ? jl[64] : smp, jsl = JOBL ? jl[192] : slot;
+        double* q = A.scratch + 3 * (((size_t)jb * A.s_count + (js - A.s_begin)) * 64 + jsl);
         q[0] = sx; q[1] = sy; q[2] = sz;
         need = true;
       } else {
