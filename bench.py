@@ -259,7 +259,8 @@ def main():
                     "achieved_kind": "modelled: algorithmic f64 FLOPs (kernel work counters x DESIGN.md FLOP model) "
                                      "/ HIP-event kernel time",
                     "traffic_source": pmc_source if world == 1 else "not measured for a shard",
-                    "kernel": "k_render<false,false,true>" if accum_ms > 0 else "k_render<false,false,false>",
+                    # k_render<HAS_MESH, BVH, STATS, DYN, EXT>: the chunked (DYN) list kernel for this frame
+                    "kernel": "k_render<false,false,false,true,false>" if accum_ms > 0 else "k_render<false,false,false,false,false>",
                     "kernel_ms": round(kern_ms, 3), "accumulate_ms": round(accum_ms, 3),
                     "algorithmic_flops_per_launch": int(flops),
                     "counts": {"samples": st.samples, "segments": st.segments, "prim_tests": st.prim_tests,
