@@ -1788,10 +1788,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // default — bitwise either way, but measured slower: cornell 4,174 vs 4,585 Msamples/s (the extra
   // code in the object loop and the deferred state cost more registers than the re-tests it saves).
   constexpr bool LPF = YART_LPF && !HAS_MESH && !BVH;
-  // JOBL (the chunked list kernels): a lane's job identity — pixel, sample, block, slot, x, y —
+  // JOBL (the chunked list and world-BVH kernels): a lane's job identity — pixel, sample, block, slot, x, y —
   // lives in LDS ([word][lane] per wave) from its hand-out to its scratch store, read where it is
   // used, instead of six VGPRs carried through every iteration.
-  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH && !BVH;
+  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH;
   __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : 1];
   __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
