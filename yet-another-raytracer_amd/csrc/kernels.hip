@@ -1794,7 +1794,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH;
   __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : 1];
   __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  // the wave index through readfirstlane: uniform, so the per-wave LDS bases live in SGPRs (as a
+  // VGPR the mesh walk's stack base was spilled and reloaded at every pop)
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // With the chunk count a multiple of 8 (capi.cpp plan()), each XCD's contiguous run of work ids
   // is whole chunks of every block: equal shares per XCD. (Without chunking the remap would give
   // one XCD all the expensive glass-sphere blocks: 1,960 vs 2,507 Msamples/s measured.)
@@ -2100,6 +2102,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       bool hit = false;
       LightCap cap;
       cap.t = &lpf_lds[128];
+      bool scat = false;
       const QueryCtx q{g.k0, g.k1, JOBL ? jl[64] : smp, JOBL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
@@ -2124,8 +2127,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           const uint32_t kind = m.kind;
           if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC ||
               (EXT && kind == YART_MAT_ISOTROPIC)) {
-            hp = h.p; hn = h.n; hmat = h.mat;  // scattered at the top of the next iteration
-            if (EXT) { hu = h.u; hv = h.v; }
+            scat = true;  // scattered at the top of the next iteration
           } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
             double emitted = 0.0;
             if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, wbin, h.p, h.u, h.v);
@@ -2134,6 +2136,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           }
         }
       }
+      // The hit to scatter next is (re)defined for every lane here, 0 where none follows: assigned
+      // only on the scatter path, it was live — and spilled — through every world pass, since the
+      // compiler cannot see that a lane which did not keep a hit starts a fresh sample instead.
+      hp = scat ? h.p : mk(0.0, 0.0, 0.0);
+      hn = scat ? h.n : mk(0.0, 0.0, 0.0);
+      hmat = scat ? h.mat : 0u;
+      if (EXT) { hu = scat ? h.u : 0.0; hv = scat ? h.v : 0.0; }
     }
     if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
       OCC(OCC_TERM);
