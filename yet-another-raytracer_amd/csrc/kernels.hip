@@ -1791,8 +1791,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // JOBL (the chunked list and world-BVH kernels): a lane's job identity — pixel, sample, block, slot, x, y —
   // lives in LDS ([word][lane] per wave) from its hand-out to its scratch store, read where it is
   // used, instead of six VGPRs carried through every iteration.
-  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH;
-  __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : 1];
+  // The mesh kernel's LDS is nearly full (36.9 KB of walk state per workgroup): it keeps three
+  // words (pixel, sample, block) and derives x, y and the slot from the pixel where needed.
+  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH, JOBL3 = YART_JOBL && DYN && HAS_MESH;
+  __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : JOBL3 ? 4 * 3 * 64 : 1];
   __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
   // the wave index through readfirstlane: uniform, so the per-wave LDS bases live in SGPRs (as a
   // VGPR the mesh walk's stack base was spilled and reloaded at every pop)
@@ -1813,7 +1815,8 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
   double* const lpf_lds = &s_lpf[LPF ? wave * 256 + lane : 0];
-  uint32_t* const jl = &s_job[JOBL ? wave * 6 * 64 + lane : 0];
+  uint32_t* const jl = &s_job[JOBL ? wave * 6 * 64 + lane : JOBL3 ? wave * 3 * 64 + lane : 0];
+  constexpr bool JL = JOBL || JOBL3;
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
   Stats st;
@@ -1885,6 +1888,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           pixel = y * W + x;
           lane_blk = local_blk;
           if (JOBL) { jl[0] = pixel; jl[64] = smp; jl[128] = lane_blk; jl[192] = slot; jl[256] = x; jl[320] = y; }
+          if (JOBL3) { jl[0] = pixel; jl[64] = smp; jl[128] = lane_blk; }
           // a pixel outside the crop grid is skipped: the lane asks again
           if ((cov >> slot) & 1ull) { fresh = true; need = false; }
         }
@@ -1936,12 +1940,15 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
-      rng_phase<!HAS_MESH && !BVH>(g, JOBL ? jl[0] : pixel, JOBL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
+      rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
       if (fresh) {  // main.rs:692-698
         OCC(OCC_FRESH);
-        const double tx = (double)(JOBL ? jl[256] : x) + gen_f64(g);
+        uint32_t jx = x, jy = y;
+        if (JOBL) { jx = jl[256]; jy = jl[320]; }
+        if (JOBL3) { const uint32_t p = jl[0]; jy = p / W; jx = p - jy * W; }
+        const double tx = (double)jx + gen_f64(g);
         const double u = tx / (double)(W - 1);
-        const double ty = (double)(JOBL ? jl[320] : y) + gen_f64(g);
+        const double ty = (double)jy + gen_f64(g);
         const double v = 1.0 - ty / (double)(H - 1);
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
 #ifndef YART_NO_LAUNDER
@@ -2079,7 +2086,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         FastMath fm;
         scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
-          rng_phase<!HAS_MESH && !BVH>(g, JOBL ? jl[0] : pixel, JOBL ? jl[64] : smp, A.max_depth - depth + 1u);
+          rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, A.max_depth - depth + 1u);
           Ieee im;
           scatter(im, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         }
@@ -2103,7 +2110,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       LightCap cap;
       cap.t = &lpf_lds[128];
       bool scat = false;
-      const QueryCtx q{g.k0, g.k1, JOBL ? jl[64] : smp, JOBL ? jl[0] : pixel, A.max_depth - depth + 1u};
+      const QueryCtx q{g.k0, g.k1, JL ? jl[64] : smp, JL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       } else if (want) {
@@ -2157,7 +2164,12 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
       if (STATS) st.v[ST_SAMPLES]++;
       if (DYN) {  // chunked: k_accumulate adds the samples in order
-        const uint32_t jb = JOBL ? jl[128] : lane_blk, js = JOBL ? jl[64] : smp, jsl = JOBL ? jl[192] : slot;
+        const uint32_t jb = JL ? jl[128] : lane_blk, js = JL ? jl[64] : smp;
+        uint32_t jsl = JOBL ? jl[192] : slot;
+        if (JOBL3) {  // the 8x8 blocks start at multiples of 8
+          const uint32_t p = jl[0], py = p / W, px = p - py * W;
+          jsl = (py & 7u) * 8u + (px & 7u);
+        }
         double* q = A.scratch + 3 * (((size_t)jb * A.s_count + (js - A.s_begin)) * 64 + jsl);
         q[0] = sx; q[1] = sy; q[2] = sz;
         need = true;
