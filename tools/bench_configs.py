@@ -17,6 +17,8 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
 sys.path.insert(0, str(ROOT / "tests"))
 import yart  # noqa: E402
+sys.path.insert(0, str(ROOT))
+from bench import FLOPS, F64_VALU_PEAK_TFLOPS, HBM_PEAK_GBS  # noqa: E402  (the FLOP model of DESIGN.md)
 
 CONFIGS = {
     "C1": ("two-spheres", 400, 225, 16, 8),
@@ -30,7 +32,9 @@ CONFIGS = {
 def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False):
     p = yart.Preset(scene_name)
     cam = p.camera(w, h)
+    ts = time.perf_counter()
     s = yart.DeviceScene(p)
+    scene_s = time.perf_counter() - ts  # host build (QBVH, world BVH) + upload, once per scene
     out = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda:0")
     st = torch.cuda.current_stream()
     s.render_async(cam, yart.render_params(w, h, 1, depth, shard_index=shard[0], shard_count=shard[1]),
@@ -48,7 +52,9 @@ def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False)
     n = w * h * spp // shard[1]
     line = {"config": name, "scene": scene_name, "stand_in": p.stand_in or None, "size": f"{w}x{h}x{spp}",
             "depth": depth, "shard": f"{shard[0]}/{shard[1]}", "kernel_ms": round(ms, 2), "wall_s": round(wall, 3),
-            "Msamples_per_s": round(n / (ms * 1e-3) / 1e6, 2)}
+            "Msamples_per_s": round(n / (ms * 1e-3) / 1e6, 2), "scene_create_s": round(scene_s, 3),
+            # end to end: scene creation (build + upload) + the frame
+            "Msamples_per_s_with_scene": round(n / (ms * 1e-3 + scene_s) / 1e6, 2)}
     if stats:
         _, c = s.render_with_stats(cam, prm)
         line["counts"] = {"samples": c.samples, "segments": c.segments, "prim_tests": c.prim_tests,
@@ -64,6 +70,28 @@ def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False)
             b = 128 * c.node_visits + 48 * c.leaf_tris + 72 * c.segments
             line["traversal_bytes"] = b
             line["traversal_GBps"] = round(b / (ms * 1e-3) / 1e9, 1)
+        # Both rooflines. FLOP side: the work counters x bench.py's per-operation FLOP
+        # model (modelled). Byte side: SURVEY's algorithmic bytes of the records the walk reads —
+        # mesh 128 B per inner node visit + 36 B per tested triangle + 60 B of closest-hit
+        # attributes per segment (an upper bound: every segment counted), world-BVH 48 B per node,
+        # list primitives 24 B per test and per light re-test — plus 48 B per sample of
+        # chunked-path scratch (written by k_render, read by k_accumulate; 0 when fused). For the
+        # mesh configs the bound is the larger fraction (SURVEY: HBM-bound traversal); the list
+        # scenes' records are a few KB that live in the scalar/L1 caches, so their bound is VALU
+        # issue whatever the byte fraction says (SURVEY: "unattainable by construction").
+        flops = (c.samples * FLOPS["sample"] + c.segments * FLOPS["segment"] + c.prim_tests * FLOPS["prim"] +
+                 c.node_visits * FLOPS["node"] + c.leaf_tris * FLOPS["leaf_tri"] + c.light_tests * FLOPS["light"])
+        mesh = bool(info.bvh_nodes)
+        nbytes = 128 * c.node_visits + 36 * c.leaf_tris + 60 * c.segments if mesh else 48 * c.node_visits
+        nbytes += 24 * (c.prim_tests + c.light_tests)
+        _, a_ms, frames = s.frame_timing(st.cuda_stream)  # warm-up + timed frame: accumulate time > 0 iff chunked
+        nbytes += 48 * n if frames and a_ms > 0 else 0
+        tf = flops / (ms * 1e-3) / 1e12
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        ff, bf = tf / F64_VALU_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
+        line["roofline"] = {"flop_tflops_modelled": round(tf, 3), "flop_frac": round(ff, 4),
+                            "alg_bytes": int(nbytes), "alg_GBps": round(gbs, 1), "alg_bytes_frac_of_hbm": round(bf, 4),
+                            "bound": ("hbm (algorithmic bytes)" if bf > ff else "valu (f64)") if mesh else "valu (f64)"}
     if cpu:
         import oracle_lib as O
         cspp = max(1, spp // 64)
