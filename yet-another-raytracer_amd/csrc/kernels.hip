@@ -14,6 +14,7 @@
 // stack access is bank-conflict free.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -132,14 +133,23 @@ struct Fast {
 };
 __device__ __forceinline__ bool flagged(const Fast& m) { return m.bad; }
 __device__ __forceinline__ bool flagged(const Ieee&) { return false; }
-// Default Ieee. Measured with one Fast re-run branch per scatter block (bitwise either way): cornell
-// 4,421 vs 4,581 Msamples/s, random-scene 1,085 vs 1,124, david 208 vs 210 — the kept-alive inputs
-// and the second copy of the block cost more (VGPR spills 44 vs 23) than the shorter cores save.
-#ifdef YART_FAST_MATH
-typedef Fast FastMath;
-#else
-typedef Ieee FastMath;
+// Policy per kernel, bitwise either way (the flagged re-run replays the draws on Ieee). r02
+// measurement after the register-liveness work, the Fast policy in every kernel vs Ieee in every
+// kernel: cornell (list, no EXT) 4,814 vs 4,716 Msamples/s, random-scene (world BVH) 1,464 vs
+// 1,514, david (mesh) 243.4 vs 243.3. So Fast runs where it wins, the plain list kernel; the
+// others keep Ieee (the second copy of the block costs them registers). YART_FAST_MATH forces
+// Fast everywhere, YART_FAST_LIST=0 forces Ieee everywhere.
+#ifndef YART_FAST_LIST
+#define YART_FAST_LIST 1
 #endif
+template <bool HAS_MESH, bool BVH, bool EXT>
+struct MathPolicy {
+#ifdef YART_FAST_MATH
+  typedef Fast type;
+#else
+  typedef typename std::conditional<YART_FAST_LIST && !HAS_MESH && !BVH && !EXT, Fast, Ieee>::type type;
+#endif
+};
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
 struct Ray { V3 o, d; double time, wl; };
@@ -2083,7 +2093,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         V3 no, nd;
         uint32_t ndepth;
         bool nterm, npend;
-        FastMath fm;
+        typename MathPolicy<HAS_MESH, BVH, EXT>::type fm;
         scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
           rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, A.max_depth - depth + 1u);
