@@ -66,6 +66,9 @@ def parse():
                          "the GPU box's share per GPU)")
     ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
     ap.add_argument("--spu", type=int, default=0, help="samples per work unit (0 = library's choice)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="frames alternate over this many HIP streams (2: the next frame's render fills the SIMD "
+                         "slots the previous frame's last paths leave idle; 1: strictly one after another)")
     return ap.parse_args()
 
 
@@ -157,18 +160,27 @@ def main():
     cam = preset.camera(W, H)
     prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world, samples_per_unit=a.spu)
     scene = yart.DeviceScene(preset.desc, device=local)
-    frame = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)  # rank 0: the assembled frame
-    rgba = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # Frames alternate over S streams, each with its own frame / packed / RGBA buffers (and, inside
+    # libyart, its own sample scratch and unit counter): frame k+1's persistent waves start in the
+    # SIMD slots frame k's last long paths leave idle. Every frame is still rendered, gathered and
+    # finalized whole; for N > 1 the collectives stay in step order on every rank (each gather waits
+    # for the previous step's, an event across the streams).
+    S = max(1, a.streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    stream = streams[0]
+    frames = [torch.zeros((H, W, 3), dtype=torch.float64, device=dev) for _ in range(S)]  # rank 0: assembled
+    rgbas = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(S)]
+    frame = frames[0]
     L = yart.load_device()
 
     # N > 1: the data-plane collective, chosen ONCE and identically on every rank
     collective, comm, gather, nccl_group = None, None, None, None
     if world > 1:
-        packed = torch.zeros(yart.shard_packed_len(W, H, 0, world), dtype=torch.float64, device=dev)
+        packeds = [torch.zeros(yart.shard_packed_len(W, H, 0, world), dtype=torch.float64, device=dev)
+                   for _ in range(S)]
         if rehearse:
             collective = "gather (gloo rehearsal, host copies)"
-            packed_h, frame_h = torch.zeros_like(packed, device="cpu"), torch.zeros_like(frame, device="cpu")
+            packed_h, frame_h = torch.zeros_like(packeds[0], device="cpu"), torch.zeros_like(frame, device="cpu")
             gather = PackedGather(W, H, world, rank, torch.device("cpu"))
         else:
             uid = [yart.Comm.unique_id() if rank == 0 else None]
@@ -191,35 +203,55 @@ def main():
                 gather = PackedGather(W, H, world, rank, dev)
                 collective = "gather (torch.distributed nccl, fallback)"
 
-    def step():
-        if world == 1:
-            scene.render_async(cam, prm, frame.data_ptr(), stream.cuda_stream)
-        else:
-            scene.render_packed_async(cam, prm, packed.data_ptr(), stream.cuda_stream)
-            if comm is not None:
-                comm.gather_frame_async(packed.data_ptr(), W, H, frame.data_ptr(), stream.cuda_stream)
-            elif rehearse:
-                packed_h.copy_(packed)
-                gather(packed_h, frame_h, dist)
-                if rank == 0:
-                    frame.copy_(frame_h)
-            else:
-                gather(packed, frame, dist, group=nccl_group)
-        if rank == 0:
-            rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
-                                             yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(stream.cuda_stream))
-            if rc != 0:
-                raise RuntimeError(L.yart_last_error().decode())
+    coll_done = [None]  # the previous step's collective (N > 1): the next one waits for it
 
-    for _ in range(a.warmup):
-        step()
+    def step(i, streams=streams):
+        k = i % len(streams)
+        st, frame, rgba = streams[k], frames[k], rgbas[k]
+        with torch.cuda.stream(st):
+            if world == 1:
+                scene.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
+            else:
+                packed = packeds[k]
+                scene.render_packed_async(cam, prm, packed.data_ptr(), st.cuda_stream)
+                if coll_done[0] is not None:
+                    st.wait_event(coll_done[0])
+                if comm is not None:
+                    comm.gather_frame_async(packed.data_ptr(), W, H, frame.data_ptr(), st.cuda_stream)
+                elif rehearse:
+                    packed_h.copy_(packed)
+                    gather(packed_h, frame_h, dist)
+                    if rank == 0:
+                        frame.copy_(frame_h)
+                else:
+                    gather(packed, frame, dist, group=nccl_group)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                coll_done[0] = ev
+            if rank == 0:
+                rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
+                                                 yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(st.cuda_stream))
+                if rc != 0:
+                    raise RuntimeError(L.yart_last_error().decode())
+
+    def drain_timing():
+        r = acc = n = 0
+        for st in streams:
+            r1, a1, n1 = scene.frame_timing(st.cuda_stream)
+            r, acc, n = r + r1, acc + a1, n + n1
+        return r, acc, n
+
+    # warm-up: W steps, and at least one frame on every stream (its scratch is allocated then)
+    prep = max(0, S - a.warmup)
+    for i in range(a.warmup + prep):
+        step(i)
     torch.cuda.synchronize(dev)
-    scene.frame_timing(stream.cuda_stream)  # drop the warm-up frames' events
+    drain_timing()  # drop the warm-up frames' events
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for i in range(a.steps):
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -228,9 +260,19 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    render_ms, accum_ms, frames = scene.frame_timing(stream.cuda_stream)
-    kern_ms = render_ms / max(1, frames)   # k_render average launch duration over the timed steps
-    accum_ms = accum_ms / max(1, frames)   # k_accumulate (chunked path)
+    render_ms, accum_ms, nfr = drain_timing()
+    overlap_ms = render_ms / max(1, nfr)  # k_render launch durations in the timed loop (overlapping for S > 1)
+    # The roofline's kernel time: k_render alone. With S > 1 the launches in the timed loop overlap
+    # (a launch's events bracket its wait for the slots the previous frame still holds), so the
+    # kernel's own duration is taken from 3 frames on one stream right after the timed region.
+    if S > 1:
+        for i in range(3):
+            step(i, streams=streams[:1])
+        torch.cuda.synchronize(dev)
+        render_ms, accum_ms, nfr = drain_timing()
+    kern_ms = render_ms / max(1, nfr)      # k_render average launch duration (one stream)
+    accum_ms = accum_ms / max(1, nfr)      # k_accumulate (chunked path)
+    frame = frames[(a.steps - 1) % S]      # the last timed frame
 
     frame_check = None
     if rank == 0:  # the image really is the frame: finite, non-zero, and for N > 1 bitwise one device's
@@ -262,6 +304,9 @@ def main():
                     # k_render<HAS_MESH, BVH, STATS, DYN, EXT>: the chunked (DYN) list kernel for this frame
                     "kernel": "k_render<false,false,false,true,false>" if accum_ms > 0 else "k_render<false,false,false,false,false>",
                     "kernel_ms": round(kern_ms, 3), "accumulate_ms": round(accum_ms, 3),
+                    "kernel_ms_source": ("HIP events, 3 frames on one stream after the timed region" if S > 1
+                                         else "HIP events over the timed steps"),
+                    "timed_launch_ms": round(overlap_ms, 3),
                     "algorithmic_flops_per_launch": int(flops),
                     "counts": {"samples": st.samples, "segments": st.segments, "prim_tests": st.prim_tests,
                                "light_tests": st.light_tests, "node_visits": st.node_visits,
@@ -286,6 +331,7 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
             "config": {"workload": "cornell-box 800x800x256spp depth 50 (BASELINE configs[1])", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"pixel-blocks x{world}",
+                       "streams": S, "prep_frames": prep,
                        "collective": collective, "frame_check": frame_check, "seed": yart.DEFAULT_SEED},
             "roofline": roofline, "cpu_baseline": cpu,
         }

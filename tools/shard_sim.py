@@ -22,17 +22,19 @@ def main():
     ap.add_argument("--w", type=int, default=800)
     ap.add_argument("--h", type=int, default=800)
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--all", action="store_true", help="time every shard of each N (load balance), not only shard 0")
     a = ap.parse_args()
     p = yart.Preset(a.scene)
     cam = p.camera(a.w, a.h)
     s = yart.DeviceScene(p)
     out = torch.zeros((a.h, a.w, 3), dtype=torch.float64, device="cuda:0")
     st = torch.cuda.current_stream()
-    for n in map(int, a.n.split(",")):
-        prm = yart.render_params(a.w, a.h, a.spp, 50, shard_index=0, shard_count=n, samples_per_unit=a.spu)
+    for n, k in [(n, k) for n in map(int, a.n.split(",")) for k in (range(n) if a.all else [0])]:
+        prm = yart.render_params(a.w, a.h, a.spp, 50, shard_index=k, shard_count=n, samples_per_unit=a.spu)
         s.render_async(cam, prm, out.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()
         best = 1e30
+        s.frame_timing(st.cuda_stream)  # reset the per-stream kernel times
         for _ in range(3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
@@ -40,7 +42,9 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             best = min(best, e0.elapsed_time(e1))
-        print(json.dumps({"n": n, "spu": a.spu, "shard_ms": round(best, 3),
+        r_ms, acc_ms, frames = s.frame_timing(st.cuda_stream)
+        print(json.dumps({"n": n, "shard": k, "spu": a.spu, "shard_ms": round(best, 3),
+                          "k_render_ms": round(r_ms / max(frames, 1), 3), "k_accumulate_ms": round(acc_ms / max(frames, 1), 3),
                           "predicted_Msamples_per_s": round(a.w * a.h * a.spp / (best * 1e-3) / 1e6, 1)}), flush=True)
 
 
