@@ -1,4 +1,4 @@
-"""Frames back to back on one stream vs alternating over two streams (the next frame's render fills
+"""Frames back to back on one stream vs alternating over two or three streams (the next frame's render fills
 the SIMD slots the previous frame's drain leaves idle), for the full frame and for shard 0 of N.
     python tools/pipeline_sim.py [--n 1,8] [--frames 20]"""
 import argparse
@@ -26,12 +26,12 @@ def main():
     p = yart.Preset(a.scene)
     cam = p.camera(a.w, a.h)
     s = yart.DeviceScene(p)
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream()]
     outs = [torch.zeros((a.h, a.w, 3), dtype=torch.float64, device="cuda:0") for _ in streams]
     for n in map(int, a.n.split(",")):
         prm = yart.render_params(a.w, a.h, a.spp, 50, shard_index=0, shard_count=n)
         res = {"n": n}
-        for ns in (1, 2, 1, 2):
+        for ns in (1, 2, 3, 1, 2, 3):
             for i in range(2 * ns):  # warm-up: scratch of every stream allocated
                 s.render_async(cam, prm, outs[i % ns].data_ptr(), streams[i % ns].cuda_stream)
             torch.cuda.synchronize()
@@ -42,7 +42,7 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / a.frames
             k = f"streams{ns}_ms"
             res[k] = round(min(ms, res.get(k, 1e30)), 3)
-        assert torch.equal(outs[0], outs[1])
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
         print(json.dumps(res), flush=True)
 
 
