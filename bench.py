@@ -140,6 +140,25 @@ def valu_issue(pmc):
         return None
 
 
+def fp64_issue(pmc, kern_ms):
+    """Hardware-counted FP64 work of the snapshot: SQ_INSTS_VALU_FLOPS_FP64 counts FLOPs per wave
+    instruction (add/mul/trans 1, FMA 2); x 64 lanes, exec mask not applied, so an upper bound on
+    the FP64 pipe's useful work. Plus the VALU instruction mix behind the issue-bound roofline."""
+    try:
+        lane_flops = pmc["SQ_INSTS_VALU_FLOPS_FP64"] * 64
+        f64 = sum(pmc[k] for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                   "SQ_INSTS_VALU_TRANS_F64"))
+        valu = pmc["SQ_INSTS_VALU"]
+    except KeyError:
+        return None
+    tf = lane_flops / (kern_ms * 1e-3) / 1e12
+    return {"lane_flops_per_launch": int(lane_flops), "tflops": round(tf, 3),
+            "frac": round(tf / F64_VALU_PEAK_TFLOPS, 4),
+            "valu_mix": {"f64_arith": round(f64 / valu, 4), "int32": round(pmc["SQ_INSTS_VALU_INT32"] / valu, 4),
+                         "other": round(1 - (f64 + pmc["SQ_INSTS_VALU_INT32"]) / valu, 4)},
+            "kind": "counted (PMC snapshot): f64 wave instructions x 64 lanes, inactive lanes included"}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -315,6 +334,7 @@ def main():
                     # the sample scratch k_render writes (24 B of XYZ per sample)
                     "algorithmic_bytes_per_launch": st.samples * 24 if accum_ms > 0 else None,
                     "valu_issue_busy": valu_issue(pmc) if world == 1 else None,
+                    "fp64_issued": fp64_issue(pmc, kern_ms) if world == 1 else None,
                     # wave-level VALU instructions (SQ_INSTS_VALU of the snapshot) per path segment
                     "valu_insts_per_segment": (round(pmc["SQ_INSTS_VALU"] / st.segments, 2)
                                                if world == 1 and pmc.get("SQ_INSTS_VALU") and st.segments else None)}
