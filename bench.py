@@ -1,14 +1,24 @@
 """bench.py — BASELINE.json's headline metric on MI355X.
 
 Metric: Msamples/s (W x H x spp / s) for cornell-box 800x800, 256 spp, depth 50 (configs[1]);
-ms_per_step is the wall-clock of one frame. A step = one frame of the hot path: every rank
-renders its share of 8x8-pixel blocks (block b -> rank b % N) with the HIP megakernel through the
-C ABI, and rank 0 finalizes the frame (XYZ -> sRGB RGBA8). For N > 1 each rank renders straight
-into its block-packed shard (yart_render_packed_async) and ONE RCCL gather over xGMI issued by
-libyart itself (yart_gather_frame_async: ncclGather + an unpack kernel on rank 0) assembles rank
-0's frame; torch.distributed (gloo) is only the control plane (the communicator id, barriers, the
-max-over-ranks time). Inputs (scene, BVH, camera) are resident in HBM before the timed region.
-Scaling is strong: the frame is fixed as N grows.
+ms_per_step is the wall-clock of one frame. A step = one frame of the hot path: the frame's 8x8
+pixel blocks are dealt to the N GPUs (block b -> GPU b % N), each GPU renders its blocks with the
+HIP megakernel through the C ABI, and the frame is finalized (XYZ -> sRGB RGBA8) on GPU 0. For
+N > 1 each GPU renders straight into its block-packed shard and ONE RCCL gather over xGMI issued
+by libyart itself assembles GPU 0's frame. Two ways to run N GPUs, one data path:
+
+  python bench.py --gpus N          one process drives N GPUs (yart_render_multi_async: every
+                                    device's render, the grouped ncclGather behind it and the
+                                    unpack are stream-ordered, no host wait or copy per frame)
+  torchrun --nproc-per-node N bench.py --gpus N
+                                    one process per GPU (yart_render_packed_async +
+                                    yart_gather_frame_async); torch.distributed (gloo) is only the
+                                    control plane (communicator id, barriers, max-over-ranks time)
+
+--gpus N must match the launch: N > 1 without torchrun needs N visible GPUs, and under torchrun
+WORLD_SIZE must equal N; otherwise bench.py exits non-zero rather than report another N.
+Inputs (scene, BVH, camera) are resident in HBM before the timed region. Scaling is strong: the
+frame is fixed as N grows.
 
 Also reported on the same line:
   roofline      the render kernel's average launch duration (HIP events the library records on
@@ -20,9 +30,6 @@ Also reported on the same line:
   cpu_baseline  the CPU restatement (oracle/) on this host's cores, rank 0 only, on a bounded
                 sample of the same workload (same frame at fewer spp; Msamples/s is ~spp-invariant),
                 with the host's nproc, usable CPUs and CPU model.
-
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import hashlib
@@ -159,17 +166,35 @@ def fp64_issue(pmc, kern_ms):
             "kind": "counted (PMC snapshot): f64 wave instructions x 64 lanes, inactive lanes included"}
 
 
+def launch_mode(a):
+    """(mode, world, rank, local): 'single' (one GPU), 'multi' (one process, N GPUs) or 'ranks' (one
+    process per GPU under torch.distributed.run). Exits non-zero when --gpus and the launch disagree."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) > 1 or (env_world is not None and a.gpus > 1):
+        world = int(env_world)
+        if world != a.gpus:
+            sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                     f"(torch.distributed.run --nproc-per-node {a.gpus}) or run without a launcher")
+        return "ranks", world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus < 1:
+        sys.exit(f"bench.py: --gpus {a.gpus}")
+    if a.gpus > 1:
+        have = torch.cuda.device_count()  # counts devices without initialising the GPU
+        if have < a.gpus:
+            sys.exit(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible; refusing to report another N")
+        return "multi", a.gpus, 0, 0
+    return "single", 1, 0, 0
+
+
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # Rehearsal of the N>1 path on a 1-GPU box (RCCL refuses two ranks on one device): every rank on
-    # device 0, the packed shards gathered over gloo on host copies. Never set for a real run.
-    rehearse = os.environ.get("YART_BENCH_SAME_DEVICE") == "1"
+    mode, world, rank, local = launch_mode(a)
+    # Rehearsal of the per-rank N>1 path on a 1-GPU box (RCCL refuses two ranks on one device): every
+    # rank on device 0, the packed shards gathered over gloo on host copies. Never set for a real run.
+    rehearse = mode == "ranks" and os.environ.get("YART_BENCH_SAME_DEVICE") == "1"
     if rehearse:
         local = 0
-    if world > 1:
+    if mode == "ranks":
         dist.init_process_group("gloo")  # control plane only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -177,13 +202,16 @@ def main():
 
     preset = yart.Preset(WORKLOAD["scene"])
     cam = preset.camera(W, H)
-    prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world, samples_per_unit=a.spu)
+    shard_index, shard_count = (rank, world) if mode == "ranks" else (0, 1)
+    prm = yart.render_params(W, H, spp, depth, shard_index=shard_index, shard_count=shard_count, samples_per_unit=a.spu)
     scene = yart.DeviceScene(preset.desc, device=local)
+    multi = yart.MultiScene(preset, list(range(world))) if mode == "multi" else None
     # Frames alternate over S streams, each with its own frame / packed / RGBA buffers (and, inside
     # libyart, its own sample scratch and unit counter): frame k+1's persistent waves start in the
     # SIMD slots frame k's last long paths leave idle. Every frame is still rendered, gathered and
     # finalized whole; for N > 1 the collectives stay in step order on every rank (each gather waits
-    # for the previous step's, an event across the streams).
+    # for the previous step's, an event across the streams; in the one-process path libyart orders
+    # them itself).
     S = max(1, a.streams)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     stream = streams[0]
@@ -192,9 +220,11 @@ def main():
     frame = frames[0]
     L = yart.load_device()
 
-    # N > 1: the data-plane collective, chosen ONCE and identically on every rank
+    # N > 1, one process per GPU: the data-plane collective, chosen ONCE and identically on every rank
     collective, comm, gather, nccl_group = None, None, None, None
-    if world > 1:
+    if mode == "multi":
+        collective = "ncclGather (libyart yart_render_multi_async, one process, ncclCommInitAll)"
+    if mode == "ranks":
         packeds = [torch.zeros(yart.shard_packed_len(W, H, 0, world), dtype=torch.float64, device=dev)
                    for _ in range(S)]
         if rehearse:
@@ -213,7 +243,7 @@ def main():
             t = torch.tensor([ok], dtype=torch.int32)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             if t.item():
-                collective = "ncclGather (libyart yart_gather_frame_async, RCCL)"
+                collective = "ncclGather (libyart yart_gather_frame_async, RCCL, one rank per GPU)"
             else:  # the same packets through torch's RCCL process group
                 if comm is not None:
                     comm.close()
@@ -222,14 +252,16 @@ def main():
                 gather = PackedGather(W, H, world, rank, dev)
                 collective = "gather (torch.distributed nccl, fallback)"
 
-    coll_done = [None]  # the previous step's collective (N > 1): the next one waits for it
+    coll_done = [None]  # the previous step's collective (ranks, N > 1): the next one waits for it
 
     def step(i, streams=streams):
         k = i % len(streams)
         st, frame, rgba = streams[k], frames[k], rgbas[k]
         with torch.cuda.stream(st):
-            if world == 1:
+            if mode == "single":
                 scene.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
+            elif mode == "multi":
+                multi.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
             else:
                 packed = packeds[k]
                 scene.render_packed_async(cam, prm, packed.data_ptr(), st.cuda_stream)
@@ -254,28 +286,35 @@ def main():
                     raise RuntimeError(L.yart_last_error().decode())
 
     def drain_timing():
+        """(render_ms, accumulate_ms or gather_ms, frames) summed over the frames since the last call."""
+        if mode == "multi":
+            return multi.frame_timing()
         r = acc = n = 0
         for st in streams:
             r1, a1, n1 = scene.frame_timing(st.cuda_stream)
             r, acc, n = r + r1, acc + a1, n + n1
         return r, acc, n
 
+    def sync_all():
+        for d in range(world if mode == "multi" else 1):
+            torch.cuda.synchronize(d if mode == "multi" else dev)
+
     # warm-up: W steps, and at least one frame on every stream (its scratch is allocated then)
     prep = max(0, S - a.warmup)
     for i in range(a.warmup + prep):
         step(i)
-    torch.cuda.synchronize(dev)
+    sync_all()
     drain_timing()  # drop the warm-up frames' events
-    if world > 1:
+    if mode == "ranks":
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
+    sync_all()
+    if mode == "ranks":
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if mode == "ranks":
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -287,10 +326,12 @@ def main():
     if S > 1:
         for i in range(3):
             step(i, streams=streams[:1])
-        torch.cuda.synchronize(dev)
+        sync_all()
         render_ms, accum_ms, nfr = drain_timing()
-    kern_ms = render_ms / max(1, nfr)      # k_render average launch duration (one stream)
-    accum_ms = accum_ms / max(1, nfr)      # k_accumulate (chunked path)
+    kern_ms = render_ms / max(1, nfr)      # k_render average launch duration (one stream; multi: slowest GPU)
+    accum_ms = accum_ms / max(1, nfr)      # k_accumulate (chunked path); multi: the root's gather + unpack
+    if mode == "multi":
+        gather_ms, accum_ms = accum_ms, None
     frame = frames[(a.steps - 1) % S]      # the last timed frame
 
     frame_check = None
@@ -309,20 +350,24 @@ def main():
     roofline = None
     cpu = None
     if rank == 0 and not a.no_stats:
-        _, st = scene.render_with_stats(cam, yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world))
+        # shard 0's counted work (the whole frame at N = 1) over its kernel time
+        _, st = scene.render_with_stats(cam, yart.render_params(W, H, spp, depth, shard_index=0, shard_count=world))
         flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
                  st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
         achieved = flops / (kern_ms * 1e-3) / 1e12
         pmc, pmc_source = pmc_snapshot()
         traffic = pmc.get("hbm_bytes_per_launch") if world == 1 else None
+        chunked = mode == "multi" or (accum_ms or 0) > 0
         roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / F64_VALU_PEAK_TFLOPS, 4), "traffic": traffic,
                     "achieved_kind": "modelled: algorithmic f64 FLOPs (kernel work counters x DESIGN.md FLOP model) "
-                                     "/ HIP-event kernel time",
+                                     "/ HIP-event kernel time" + ("" if world == 1 else
+                                                                   " (shard 0's work / the slowest GPU's kernel time)"),
                     "traffic_source": pmc_source if world == 1 else "not measured for a shard",
                     # k_render<HAS_MESH, BVH, STATS, DYN, EXT>: the chunked (DYN) list kernel for this frame
-                    "kernel": "k_render<false,false,false,true,false>" if accum_ms > 0 else "k_render<false,false,false,false,false>",
-                    "kernel_ms": round(kern_ms, 3), "accumulate_ms": round(accum_ms, 3),
+                    "kernel": "k_render<false,false,false,true,false>" if chunked else "k_render<false,false,false,false,false>",
+                    "kernel_ms": round(kern_ms, 3),
+                    "accumulate_ms": round(accum_ms, 3) if accum_ms is not None else None,
                     "kernel_ms_source": ("HIP events, 3 frames on one stream after the timed region" if S > 1
                                          else "HIP events over the timed steps"),
                     "timed_launch_ms": round(overlap_ms, 3),
@@ -332,12 +377,14 @@ def main():
                                "leaf_tris": st.leaf_tris},
                     "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None),
                     # the sample scratch k_render writes (24 B of XYZ per sample)
-                    "algorithmic_bytes_per_launch": st.samples * 24 if accum_ms > 0 else None,
+                    "algorithmic_bytes_per_launch": st.samples * 24 if chunked else None,
                     "valu_issue_busy": valu_issue(pmc) if world == 1 else None,
                     "fp64_issued": fp64_issue(pmc, kern_ms) if world == 1 else None,
                     # wave-level VALU instructions (SQ_INSTS_VALU of the snapshot) per path segment
                     "valu_insts_per_segment": (round(pmc["SQ_INSTS_VALU"] / st.segments, 2)
                                                if world == 1 and pmc.get("SQ_INSTS_VALU") and st.segments else None)}
+        if mode == "multi":
+            roofline["gather_ms"] = round(gather_ms, 3)
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
 
@@ -351,6 +398,8 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
             "config": {"workload": "cornell-box 800x800x256spp depth 50 (BASELINE configs[1])", "width": W,
                        "height": H, "spp": spp, "max_depth": depth, "parallelism": f"pixel-blocks x{world}",
+                       "launch": {"single": "one process, one GPU", "multi": "one process, N GPUs",
+                                  "ranks": "one process per GPU (torch.distributed.run)"}[mode],
                        "streams": S, "prep_frames": prep,
                        "collective": collective, "frame_check": frame_check, "seed": yart.DEFAULT_SEED},
             "roofline": roofline, "cpu_baseline": cpu,
@@ -358,7 +407,9 @@ def main():
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
-    if world > 1:
+    if multi is not None:
+        multi.close()
+    if mode == "ranks":
         dist.destroy_process_group()
 
 

@@ -267,7 +267,8 @@ int yart_frame_timing(yart_scene* scene, void* hip_stream, double* render_ms, do
 
 /* Same, with host output and an optional progress callback, called on this thread while the
  * device renders (every ~10 ms when the count moved): pixels_done is monotone, counts the covered
- * pixels of the shard whose work has been handed out, and the last call reports all of them. */
+ * pixels of the shard whose work has been handed out (chunked plan) or finished (fused plan), and
+ * the last call reports all of them. */
 int yart_render(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
                 double* xyz_sum_out, yart_progress_fn progress, void* user);
 
@@ -316,17 +317,41 @@ int yart_gather_frame_async(yart_comm* comm, const double* d_packed, uint32_t wi
                             int root, double* d_frame, void* hip_stream);
 
 /* One process driving N devices: a scene resident on each (uploaded once) and an RCCL
- * communicator over them. yart_render_multi renders shard d on device d (all devices at once, each
- * on its own stream), gathers the shards to devices[0] and copies the frame to host memory:
- * bitwise yart_render on one device. Progress (if any) counts pixels over all devices and runs on
- * the calling thread. p->shard_index / shard_count are ignored (the devices are the shards). */
+ * communicator over them (ncclCommInitAll). p->shard_index / shard_count are ignored (device d
+ * renders shard d of N).
+ *
+ * yart_render_multi_async is the timed multi-GPU path (bench.py --gpus N without a launcher):
+ * every device renders its shard into a packed buffer on a stream of the multi's own, the
+ * grouped ncclGather is enqueued right behind each device's render (stream order, no host wait)
+ * and devices[0] unpacks the frame into d_frame (width*height*3 doubles on devices[0]) after the
+ * work already queued on `hip_stream` (a stream of devices[0]), which then waits for the frame.
+ * Frames submitted on different caller streams overlap on the devices; their gathers run in
+ * submission order on every device. Bitwise yart_render on one device: each pixel has one writer.
+ *
+ * yart_render_multi is the same submission with host output and an optional progress callback
+ * (pixels over all devices, on the calling thread); it waits for the frame and copies it to
+ * xyz_sum_out. */
 typedef struct yart_multi yart_multi;
 int yart_multi_create(int n_devices, const int* devices, const yart_scene_desc* desc, yart_multi** out);
+int yart_render_multi_async(yart_multi* m, const yart_camera* cam, const yart_render_params* p,
+                            double* d_frame, void* hip_stream);
 int yart_render_multi(yart_multi* m, const yart_camera* cam, const yart_render_params* p,
                       double* xyz_sum_out, yart_progress_fn progress, void* user);
+/* Device time of the frames submitted with yart_render_multi_async since the previous call (call
+ * once they have finished): the slowest device's summed render-kernel time, the root's summed
+ * gather + unpack time (from the root's gather launch, so it includes waiting for the slowest
+ * device) and the number of frames. */
+int yart_multi_frame_timing(yart_multi* m, double* render_ms, double* gather_ms, uint32_t* frames);
 /* Device time of the last yart_render_multi: render (slowest device) and gather + unpack, ms. */
 int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gather_ms);
 void yart_multi_destroy(yart_multi* m);
+
+/* The root side of the gather on its own (k_unpack_shards): `shards` packets back to back in
+ * d_recv, packet r (shard r's packed buffer) at r * stride doubles, stride >= the largest shard's
+ * yart_shard_packed_len -> the whole frame in d_frame (0 outside the crop grid). Device buffers,
+ * caller stream. Lets a caller that moves packets by other means (or a test) assemble frames. */
+int yart_unpack_shards_async(int device, const double* d_recv, uint32_t shards, uint64_t stride,
+                             uint32_t width, uint32_t height, double* d_frame, void* hip_stream);
 
 /* main.rs:710-718: xyz * 360 / (CIE_Y_INTERGAL * spp) -> XYZ::into_rgb -> sRGB gamma ->
  * (256 * clamp(c, 0, 0.999)) as u8, alpha 255; pixels the tile grid never covers -> 0,0,0,0.

@@ -68,3 +68,30 @@ def test_kernel_time_agrees_with_rocprof_stats():
     rocprof_ms = float(rows[0]["AverageNs"]) * 1e-6
     # rocprof averages the overlapped two-stream launches with the solo ones: a few %
     assert b["roofline"]["kernel_ms"] == pytest.approx(rocprof_ms, rel=0.05)
+
+
+def _run_bench(args, env_extra):
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    env["HIP_VISIBLE_DEVICES"] = env.get("HIP_VISIBLE_DEVICES", "")  # never touch a GPU from this test
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=env,
+                          timeout=300, cwd=str(ROOT))
+
+
+@pytest.mark.parametrize("args,env", [
+    (["--gpus", "2", "--steps", "1", "--warmup", "0"], {}),                       # 2 GPUs asked, none visible
+    (["--gpus", "8", "--steps", "1", "--warmup", "0"], {}),
+    (["--gpus", "4", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}),
+    (["--gpus", "2", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}),
+])
+def test_gpus_flag_never_reports_another_n(args, env):
+    """--gpus N either drives N GPUs (one process over N devices, or N ranks under
+    torch.distributed.run) or exits non-zero: a launch that does not match N must never print a
+    bench line (`--gpus` was parsed and ignored, reporting n_gpus 1)."""
+    r = _run_bench(args, env)
+    assert r.returncode != 0, r.stdout
+    assert '"n_gpus"' not in r.stdout
+    assert "bench.py: --gpus" in r.stderr

@@ -8,6 +8,7 @@ fan-out + stitching of tile results (main.rs:633-660, 747-760), and `raytracer -
 (main.rs:777-781)."""
 import os
 import subprocess
+import sys
 import threading
 
 import numpy as np
@@ -139,6 +140,66 @@ def test_render_multi_on_one_device_is_the_render():
     assert r > 0 and g >= 0
     assert calls[-1] == int(O.coverage(W, H).sum())
     m.close()
+
+
+def test_render_multi_async_on_one_device_is_the_render():
+    """yart_render_multi_async (bench.py's one-process N-GPU path) at n = 1: renders, grouped
+    ncclGather and unpack enqueued without a host wait, frames alternating over two caller
+    streams - every frame bitwise yart_render; the timing covers every frame."""
+    p = yart.Preset("cornell-box")
+    W, H, spp = 72, 40, 8
+    cam = p.camera(W, H)
+    prm = yart.render_params(W, H, spp, 50)
+    ref = yart.DeviceScene(p).render(cam, prm)
+    m = yart.MultiScene(p, [0])
+    sts = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    frames = [torch.full((H, W, 3), float("nan"), dtype=torch.float64, device="cuda:0") for _ in range(2)]
+    for i in range(5):
+        with torch.cuda.stream(sts[i % 2]):
+            m.render_async(cam, prm, frames[i % 2].data_ptr(), sts[i % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for f in frames:
+        np.testing.assert_array_equal(f.cpu().numpy(), ref)
+    r, g, n = m.frame_timing()
+    assert n == 5 and r > 0 and g > 0
+    m.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_unpack_of_n_packed_shards_is_the_render(n):
+    """The root side of the N-rank gather without the transport: shard k rendered by
+    yart_render_packed_async into slot k of ONE buffer whose slots are shard 0's packet length
+    apart (ncclGather's equal-sized packets), then yart_unpack_shards_async - bitwise the plain
+    render. Ragged W and H, so shard 0 holds more blocks than the others; the tails of the smaller
+    shards' slots are NaN and must never be read. (The multi-device RCCL transport itself runs only
+    on the driver's 8-GPU node.)"""
+    p = yart.Preset("cornell-box")
+    s = yart.DeviceScene(p)
+    W, H, spp = 52, 36, 4  # 7 x 5 = 35 blocks
+    cam = p.camera(W, H)
+    full = s.render(cam, yart.render_params(W, H, spp, 50))
+    stride = yart.shard_packed_len(W, H, 0, n)
+    assert stride > yart.shard_packed_len(W, H, n - 1, n)
+    recv = torch.full((n * stride,), float("nan"), dtype=torch.float64, device="cuda:0")
+    st = torch.cuda.current_stream()
+    for k in range(n):
+        s.render_packed_async(cam, yart.render_params(W, H, spp, 50, shard_index=k, shard_count=n),
+                              recv.data_ptr() + 8 * k * stride, st.cuda_stream)
+    frame = torch.full((H, W, 3), float("nan"), dtype=torch.float64, device="cuda:0")
+    yart.unpack_shards_async(0, recv.data_ptr(), n, stride, W, H, frame.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(frame.cpu().numpy(), full)
+
+
+def test_bench_gpus_beyond_the_box_exits_nonzero(repo):
+    """On a 1-GPU box, `bench.py --gpus 2` (the driver's command form) refuses instead of
+    reporting a 1-GPU number."""
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-stats", "--cpu-spp", "0"], capture_output=True, text=True, timeout=300, cwd=str(repo))
+    if torch.cuda.device_count() >= 2:
+        assert r.returncode == 0 and '"n_gpus": 2' in r.stdout, r.stderr
+    else:
+        assert r.returncode != 0 and '"n_gpus"' not in r.stdout
 
 
 def test_cli_end_to_end(tmp_path, repo):

@@ -8,7 +8,10 @@
 #include <thread>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
+#include <new>
+#include <system_error>
 
 namespace yart_dev {
 namespace {
@@ -16,6 +19,24 @@ namespace {
 struct Box {
   double mn[3], mx[3];
 };
+
+// Runs tasks[0] on this thread and the others on threads of their own where the system gives one;
+// a task whose thread cannot be created (std::system_error) runs here instead, so no exception
+// leaves the C ABI and the result is the same either way.
+void run_all(std::vector<std::function<void()>>& tasks) {
+  std::vector<std::thread> th;
+  std::vector<size_t> inline_tasks;
+  for (size_t i = 1; i < tasks.size(); ++i) {
+    try {
+      th.emplace_back(tasks[i]);
+    } catch (const std::system_error&) {
+      inline_tasks.push_back(i);
+    }
+  }
+  if (!tasks.empty()) tasks[0]();
+  for (size_t i : inline_tasks) tasks[i]();
+  for (auto& t : th) t.join();
+}
 
 // ORDER_TABLE (qbvh.rs:14-16) row for a node's split axes (top | left << 2 | right << 4) and a
 // ray octant (x >= 0 | y >= 0 << 1 | z >= 0 << 2): four nibbles, the child pushed k-th in nibble k
@@ -104,16 +125,16 @@ struct Builder {
     if (parts < 2) { std::sort(first, last, less); return; }
     std::vector<size_t> cut(parts + 1);
     for (uint32_t p = 0; p <= parts; ++p) cut[p] = n * p / parts;
-    std::vector<std::thread> th;
-    for (uint32_t p = 0; p < parts; ++p) th.emplace_back([&, p] { std::sort(first + cut[p], first + cut[p + 1], less); });
-    for (auto& t : th) t.join();
+    std::vector<std::function<void()>> tasks;
+    for (uint32_t p = 0; p < parts; ++p) tasks.emplace_back([&, p] { std::sort(first + cut[p], first + cut[p + 1], less); });
+    run_all(tasks);
     for (uint32_t w = 1; w < parts; w *= 2) {  // pairwise merges, each round in parallel
-      th.clear();
+      tasks.clear();
       for (uint32_t p = 0; p + w < parts; p += 2 * w) {
         const size_t a = cut[p], m = cut[p + w], b = cut[std::min(p + 2 * w, parts)];
-        th.emplace_back([=] { std::inplace_merge(first + a, first + m, first + b, less); });
+        tasks.emplace_back([=] { std::inplace_merge(first + a, first + m, first + b, less); });
       }
-      for (auto& t : th) t.join();
+      run_all(tasks);
     }
   }
 
@@ -168,11 +189,9 @@ struct Builder {
     }
     Result ch[4];
     if (level < par_levels) {
-      std::thread th[3];
-      for (int k = 1; k < 4; ++k)
-        th[k - 1] = std::thread([&, k] { ch[k] = construct(qo[k], qn[k], level + 1, nb[k], lb[k]); });
-      ch[0] = construct(qo[0], qn[0], level + 1, nb[0], lb[0]);
-      for (auto& t : th) t.join();
+      std::vector<std::function<void()>> tasks;
+      for (int k = 0; k < 4; ++k) tasks.emplace_back([&, k] { ch[k] = construct(qo[k], qn[k], level + 1, nb[k], lb[k]); });
+      run_all(tasks);
     } else {
       for (int k = 0; k < 4; ++k) ch[k] = construct(qo[k], qn[k], level + 1, nb[k], lb[k]);
     }
@@ -237,8 +256,8 @@ void rank_leaves(BuiltMesh& m, uint32_t root) {
 
 }  // namespace
 
-bool build_qbvh(uint32_t n, const float* positions, const double* normals, BuiltMesh& out, std::string& err,
-                const QbvhOptions& opt) {
+static bool build_qbvh_impl(uint32_t n, const float* positions, const double* normals, BuiltMesh& out, std::string& err,
+                     const QbvhOptions& opt) {
   const auto t0 = std::chrono::steady_clock::now();
   if (n <= 4) {
     err = "mesh has <= 4 triangles: the reference's L4QBVH::hit cannot traverse it (qbvh.rs:383-384)";
@@ -279,10 +298,10 @@ bool build_qbvh(uint32_t n, const float* positions, const double* normals, Built
   };
   {
     const uint32_t parts = std::min<uint32_t>(threads, std::max<uint32_t>(1u, n / 16384u));
-    std::vector<std::thread> th;
-    for (uint32_t p = 1; p < parts; ++p) th.emplace_back(prep, (uint32_t)((uint64_t)n * p / parts), (uint32_t)((uint64_t)n * (p + 1) / parts));
-    prep(0, (uint32_t)((uint64_t)n / parts));
-    for (auto& t : th) t.join();
+    std::vector<std::function<void()>> tasks;
+    for (uint32_t p = 0; p < parts; ++p)
+      tasks.emplace_back([&, p] { prep((uint32_t)((uint64_t)n * p / parts), (uint32_t)((uint64_t)n * (p + 1) / parts)); });
+    run_all(tasks);
   }
   SizeTable st;
   const Sizes total = st.get(n);
@@ -304,6 +323,18 @@ bool build_qbvh(uint32_t n, const float* positions, const double* normals, Built
     return false;
   }
   return true;
+}
+
+bool build_qbvh(uint32_t n, const float* positions, const double* normals, BuiltMesh& out, std::string& err,
+                const QbvhOptions& opt) {
+  try {  // nothing may unwind across the C ABI
+    return build_qbvh_impl(n, positions, normals, out, err, opt);
+  } catch (const std::bad_alloc&) {
+    err = "out of host memory building the QBVH";
+  } catch (const std::exception& e) {
+    err = std::string("QBVH build failed: ") + e.what();
+  }
+  return false;
 }
 
 }  // namespace yart_dev

@@ -533,7 +533,7 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
   StreamState* st = stream_state(s, stream);
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
-  if (prog) a.progress = prog->device;
+  if (prog) { a.progress = prog->device; a.progress_count = prog->counter; }
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
     if (prog) prog->total_units = a.n_blocks;
     if (int rc = take_events(s, 2, ev)) return rc;
@@ -605,11 +605,22 @@ int alloc_progress(Progress& p) {
   hipError_t e = hipHostGetDevicePointer(&d, h, 0);
   if (e != hipSuccess) { (void)hipHostFree(h); p.host = nullptr; return hip_fail(e, "hipHostGetDevicePointer"); }
   p.device = static_cast<uint32_t*>(d);
+  void* c = nullptr;
+  e = hipMalloc(&c, 4);
+  if (e == hipSuccess) e = hipMemset(c, 0, 4);
+  if (e != hipSuccess) {
+    if (c) (void)hipFree(c);
+    (void)hipHostFree(h);
+    p.host = p.device = nullptr;
+    return hip_fail(e, "hipMalloc progress counter");
+  }
+  p.counter = static_cast<uint32_t*>(c);
   return YART_OK;
 }
 void free_progress(Progress& p) {
   if (p.host) (void)hipHostFree(p.host);
-  p.host = p.device = nullptr;
+  if (p.counter) (void)hipFree(p.counter);
+  p.host = p.device = p.counter = nullptr;
 }
 
 int wait_with_progress(const std::vector<hipEvent_t>& done, const std::vector<int>& devices,

@@ -28,6 +28,8 @@ struct RenderArgs {
   uint32_t packed;    // out is block-packed: [local_blk][slot][xyz] (yart_render_packed_async)
   uint32_t progress_base;     // units of earlier passes of this frame
   uint32_t* progress;         // host-mapped word (null = none): a plain store of base + units claimed
+                              // (chunked path) or finished (fused path)
+  uint32_t* progress_count;   // fused path with progress: device counter of finished units (zeroed per frame)
 };
 
 // Shard s of N owns global blocks s, s + N, s + 2N, ... of the ceil(W/8) x ceil(H/8) grid.

@@ -2195,8 +2195,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     double* o = A.out + 3 * (A.packed ? (size_t)local_blk * 64 + lane : (size_t)pixel);
     o[0] = acc0; o[1] = acc1; o[2] = acc2;
   }
-  if (!DYN && A.progress && lane == 0)
-    __hip_atomic_store(A.progress, A.progress_base + (blockIdx.x + 1u) * 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!DYN && A.progress && lane == 0) {  // units finished so far: a counter, whatever order waves end in
+    const uint32_t done = atomicAdd(A.progress_count, 1u) + 1u;
+    __hip_atomic_store(A.progress, A.progress_base + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (STATS) {
     for (int i = 0; i < kNumStats; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);

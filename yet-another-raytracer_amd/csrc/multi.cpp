@@ -11,7 +11,9 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -126,29 +128,242 @@ int yart_gather_frame_async(yart_comm* c, const double* d_packed, uint32_t w, ui
 
 }  // extern "C"
 
+
+// ------------------------------------------------------------ one process, N devices
+// A slot is what the frames submitted on one caller stream use: a stream, a packed shard and a
+// gather event per device, and the root's receive buffer. Frames on different caller streams
+// overlap (the next frame's renders take the SIMD slots the previous frame's drain leaves idle);
+// the gathers still run in submission order on every device (each waits for the previous
+// submission's gather on its device), which is the order RCCL needs on a communicator.
+struct MultiSlot {
+  std::vector<hipStream_t> streams;   // per device, library-owned, non-blocking
+  std::vector<double*> packed;        // per device, packet_len doubles
+  std::vector<size_t> packed_bytes;
+  std::vector<hipEvent_t> gathered;   // per device: its ncclGather of the latest frame
+  hipEvent_t start = nullptr;         // devices[0]: the caller stream's work before the frame
+  hipEvent_t done = nullptr;          // devices[0]: the frame unpacked
+  double* recv = nullptr;             // devices[0]: every shard's packet
+  size_t recv_bytes = 0;
+  // devices[0]: the root's gather + unpack interval of each frame not yet read (timing)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_events;
+};
+
 struct yart_multi {
   int n = 0;
   std::vector<int> devices;
   std::vector<yart_scene*> scenes;
   std::vector<yart_comm*> comms;
-  std::vector<hipStream_t> streams;
-  std::vector<double*> packed;  // per device, packet_len doubles (grown on demand)
-  std::vector<size_t> packed_bytes;
-  double* frame = nullptr;      // on devices[0]
+  std::mutex mu;                                   // submissions are enqueued one at a time
+  std::map<hipStream_t, std::unique_ptr<MultiSlot>> slots;  // by caller stream (devices[0])
+  std::vector<hipEvent_t> last_gather;             // per device: the latest submission's gather
+  hipStream_t host_stream = nullptr;               // devices[0]: yart_render_multi's caller stream
+  double* frame = nullptr;                         // devices[0]: yart_render_multi's frame
   size_t frame_bytes = 0;
-  double render_ms = 0.0, gather_ms = 0.0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_pool;  // devices[0]: recycled timing pairs
+  double render_ms = 0.0, gather_ms = 0.0;  // yart_render_multi's last frame
   ~yart_multi() {
-    for (int d = 0; d < n; ++d) {
+    for (int d = 0; d < n && d < (int)devices.size(); ++d) {
       (void)hipSetDevice(devices[(size_t)d]);
-      if ((size_t)d < streams.size() && streams[(size_t)d]) (void)hipStreamSynchronize(streams[(size_t)d]);
-      if ((size_t)d < packed.size() && packed[(size_t)d]) (void)hipFree(packed[(size_t)d]);
-      if (d == 0 && frame) (void)hipFree(frame);
-      if ((size_t)d < streams.size() && streams[(size_t)d]) (void)hipStreamDestroy(streams[(size_t)d]);
+      for (auto& kv : slots) {
+        MultiSlot& s = *kv.second;
+        if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamSynchronize(s.streams[(size_t)d]);
+      }
+    }
+    for (int d = 0; d < n && d < (int)devices.size(); ++d) {
+      (void)hipSetDevice(devices[(size_t)d]);
+      for (auto& kv : slots) {
+        MultiSlot& s = *kv.second;
+        if ((size_t)d < s.packed.size() && s.packed[(size_t)d]) (void)hipFree(s.packed[(size_t)d]);
+        if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
+        if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamDestroy(s.streams[(size_t)d]);
+        if (d == 0) {
+          for (auto& e : s.gather_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+          if (s.recv) (void)hipFree(s.recv);
+          if (s.start) (void)hipEventDestroy(s.start);
+          if (s.done) (void)hipEventDestroy(s.done);
+        }
+      }
+      if (d == 0) {
+        for (auto& e : gather_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+        if (frame) (void)hipFree(frame);
+        if (host_stream) { (void)hipStreamSynchronize(host_stream); (void)hipStreamDestroy(host_stream); }
+      }
     }
     for (yart_comm* c : comms) delete c;
     for (yart_scene* s : scenes) yart_scene_destroy(s);
   }
 };
+
+namespace {
+
+struct RestoreDevice {
+  int d = 0;
+  RestoreDevice() { (void)hipGetDevice(&d); }
+  ~RestoreDevice() { (void)hipSetDevice(d); }
+};
+
+// The slot of a caller stream, created on first use (streams and events made once, reused).
+int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
+  auto& e = m->slots[caller];
+  if (!e) {
+    auto s = std::make_unique<MultiSlot>();
+    s->streams.assign((size_t)m->n, nullptr);
+    s->packed.assign((size_t)m->n, nullptr);
+    s->packed_bytes.assign((size_t)m->n, 0);
+    s->gathered.assign((size_t)m->n, nullptr);
+    for (int d = 0; d < m->n; ++d) {
+      HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
+      HIP_TRY(hipStreamCreateWithFlags(&s->streams[(size_t)d], hipStreamNonBlocking), "hipStreamCreate");
+      HIP_TRY(hipEventCreateWithFlags(&s->gathered[(size_t)d], hipEventDisableTiming), "hipEventCreate");
+      if (d == 0) {
+        HIP_TRY(hipEventCreateWithFlags(&s->start, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming), "hipEventCreate");
+      }
+    }
+    e = std::move(s);
+  }
+  *out = e.get();
+  return YART_OK;
+}
+
+int gather_event_pair(yart_multi* m, std::pair<hipEvent_t, hipEvent_t>& out) {  // on devices[0]
+  if (!m->gather_pool.empty()) {
+    out = m->gather_pool.back();
+    m->gather_pool.pop_back();
+    return YART_OK;
+  }
+  HIP_TRY(hipEventCreate(&out.first), "hipEventCreate");
+  if (hipError_t e = hipEventCreate(&out.second)) { (void)hipEventDestroy(out.first); return hip_fail(e, "hipEventCreate"); }
+  return YART_OK;
+}
+
+// Enqueue one frame: every device renders its shard into its packed buffer on the slot's stream,
+// the grouped ncclGather follows each render in stream order, and devices[0] unpacks into
+// d_frame after the caller stream's earlier work; the caller stream then waits for the frame.
+// No host wait. prog: one progress word per device, or null.
+int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params* p, double* d_frame, hipStream_t caller,
+                 std::vector<Progress>* prog) {
+  if (!cam || !p || !d_frame) return fail(YART_ERR_INVALID, "null argument");
+  if (p->width == 0 || p->height == 0) return fail(YART_ERR_INVALID, "width and height must be > 0");
+  const int n = m->n;
+  const uint32_t W = p->width, H = p->height;
+  const uint64_t stride = packet_len(W, H, (uint32_t)n);
+  const size_t pk_bytes = sizeof(double) * stride;
+  RestoreDevice restore;
+  MultiSlot* S = nullptr;
+  if (int rc = multi_slot(m, caller, &S)) return rc;
+  // 1. renders, one per device, each straight into its packed shard
+  for (int d = 0; d < n; ++d) {
+    const size_t di = (size_t)d;
+    HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
+    hipStream_t st = S->streams[di];
+    if (S->packed_bytes[di] < pk_bytes) {
+      if (S->packed[di]) {
+        HIP_TRY(hipStreamSynchronize(st), "drain");
+        HIP_TRY(hipFree(S->packed[di]), "hipFree");
+      }
+      S->packed[di] = nullptr; S->packed_bytes[di] = 0;
+      HIP_TRY(hipMalloc(&S->packed[di], pk_bytes), "hipMalloc packed shard");
+      // a smaller shard sends its tail too (equal-sized packets); zeroed once, never read
+      HIP_TRY(hipMemsetAsync(S->packed[di], 0, pk_bytes, st), "hipMemset");
+      S->packed_bytes[di] = pk_bytes;
+    }
+    RenderArgs a;
+    yart_render_params q = *p;
+    q.shard_index = (uint32_t)d;
+    q.shard_count = (uint32_t)n;
+    if (int rc = make_args(m->scenes[di], cam, &q, S->packed[di], a)) return rc;
+    a.packed = 1;
+    Progress* pr = prog ? &(*prog)[di] : nullptr;
+    if (int rc = launch_frame(m->scenes[di], a, p->samples_per_unit, false, st, pr)) return rc;
+  }
+  // 2. the root's receive buffer (per slot: a later slot's gather may land while this one unpacks)
+  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
+  if (S->recv_bytes < pk_bytes * (size_t)n) {
+    if (S->recv) {
+      HIP_TRY(hipStreamSynchronize(S->streams[0]), "drain");
+      HIP_TRY(hipFree(S->recv), "hipFree");
+    }
+    S->recv = nullptr; S->recv_bytes = 0;
+    HIP_TRY(hipMalloc(&S->recv, pk_bytes * (size_t)n), "hipMalloc gather buffer");
+    S->recv_bytes = pk_bytes * (size_t)n;
+  }
+  std::pair<hipEvent_t, hipEvent_t> gev;
+  if (int rc = gather_event_pair(m, gev)) return rc;
+  S->gather_events.push_back(gev);
+  // 3. ONE gather to devices[0], each device's part right behind its render; in submission order
+  for (int d = 0; d < n; ++d) {
+    const size_t di = (size_t)d;
+    HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
+    if (m->last_gather[di] && m->last_gather[di] != S->gathered[di])
+      HIP_TRY(hipStreamWaitEvent(S->streams[di], m->last_gather[di], 0), "hipStreamWaitEvent");
+    if (d == 0) HIP_TRY(hipEventRecord(gev.first, S->streams[0]), "hipEventRecord");
+  }
+  NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
+  for (int d = 0; d < n; ++d) {
+    const size_t di = (size_t)d;
+    (void)hipSetDevice(m->devices[di]);
+    ncclResult_t r = ncclGather(S->packed[di], d == 0 ? S->recv : nullptr, stride, ncclFloat64, 0, m->comms[di]->comm,
+                                S->streams[di]);
+    if (r != ncclSuccess) { (void)ncclGroupEnd(); return nccl_fail(r, "ncclGather"); }
+  }
+  NCCL_TRY(ncclGroupEnd(), "ncclGroupEnd");
+  for (int d = 0; d < n; ++d) {
+    const size_t di = (size_t)d;
+    HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
+    HIP_TRY(hipEventRecord(S->gathered[di], S->streams[di]), "hipEventRecord");
+    m->last_gather[di] = S->gathered[di];
+  }
+  // 4. unpack on the root, after whatever the caller stream had queued (it may still read d_frame)
+  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
+  HIP_TRY(hipEventRecord(S->start, caller), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(S->streams[0], S->start, 0), "hipStreamWaitEvent");
+  HIP_TRY(launch_unpack_shards(S->recv, (uint32_t)n, stride, W, H, d_frame, S->streams[0]), "launch k_unpack_shards");
+  HIP_TRY(hipEventRecord(gev.second, S->streams[0]), "hipEventRecord");
+  HIP_TRY(hipEventRecord(S->done, S->streams[0]), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(caller, S->done, 0), "hipStreamWaitEvent");
+  return YART_OK;
+}
+
+// Summed kernel times of the frames submitted since the last read, over every slot or one
+// (their streams idle by then): render = the slowest device's summed k_render time,
+// gather = the root's gather + unpack intervals, which include the root's wait for the slowest
+// device's render to finish.
+int multi_timing(yart_multi* m, MultiSlot* only, double* render_ms, double* gather_ms, uint32_t* frames) {
+  RestoreDevice restore;
+  double worst = 0.0;
+  uint32_t nf = 0;
+  for (int d = 0; d < m->n; ++d) {
+    double r = 0.0;
+    for (auto& kv : m->slots) {
+      if (only && kv.second.get() != only) continue;
+      double rr = 0.0, acc = 0.0;
+      uint32_t f = 0;
+      if (int rc = yart_frame_timing(m->scenes[(size_t)d], kv.second->streams[(size_t)d], &rr, &acc, &f)) return rc;
+      r += rr;
+      if (d == 0) nf += f;
+    }
+    if (r > worst) worst = r;
+  }
+  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
+  double g = 0.0;
+  for (auto& kv : m->slots) {
+    if (only && kv.second.get() != only) continue;
+    for (auto& e : kv.second->gather_events) {
+      float ms = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second), "hipEventElapsedTime");
+      g += ms;
+      m->gather_pool.push_back(e);
+    }
+    kv.second->gather_events.clear();
+  }
+  *render_ms = worst;
+  *gather_ms = g;
+  *frames = nf;
+  return YART_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -164,24 +379,33 @@ int yart_multi_create(int n, const int* devices, const yart_scene_desc* desc, ya
   auto m = std::make_unique<yart_multi>();
   m->n = n;
   m->devices.assign(devices, devices + n);
-  int old = 0;
-  (void)hipGetDevice(&old);
+  m->last_gather.assign((size_t)n, nullptr);
+  RestoreDevice restore;
   for (int d = 0; d < n; ++d) {  // the scene is uploaded once per device, here
     yart_scene* s = nullptr;
     if (int rc = yart_scene_create(devices[d], desc, &s)) return rc;
     m->scenes.push_back(s);
-    hipStream_t st;
-    (void)hipSetDevice(devices[d]);
-    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    (void)hipSetDevice(old);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-    m->streams.push_back(st);
   }
+  HIP_TRY(hipSetDevice(devices[0]), "hipSetDevice");
+  HIP_TRY(hipStreamCreateWithFlags(&m->host_stream, hipStreamNonBlocking), "hipStreamCreate");
   m->comms.assign((size_t)n, nullptr);
   if (int rc = yart_comm_init_all(n, devices, m->comms.data())) return rc;
-  m->packed.assign((size_t)n, nullptr);
-  m->packed_bytes.assign((size_t)n, 0);
   *out = m.release();
+  return ok();
+}
+
+int yart_render_multi_async(yart_multi* m, const yart_camera* cam, const yart_render_params* p, double* d_frame,
+                            void* stream) {
+  if (!m) return fail(YART_ERR_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(m->mu);
+  if (int rc = multi_submit(m, cam, p, d_frame, (hipStream_t)stream, nullptr)) return rc;
+  return ok();
+}
+
+int yart_multi_frame_timing(yart_multi* m, double* render_ms, double* gather_ms, uint32_t* frames) {
+  if (!m || !render_ms || !gather_ms || !frames) return fail(YART_ERR_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(m->mu);
+  if (int rc = multi_timing(m, nullptr, render_ms, gather_ms, frames)) return rc;
   return ok();
 }
 
@@ -189,108 +413,49 @@ int yart_render_multi(yart_multi* m, const yart_camera* cam, const yart_render_p
                       yart_progress_fn progress, void* user) {
   if (!m || !cam || !p || !xyz_sum_out) return fail(YART_ERR_INVALID, "null argument");
   if (p->width == 0 || p->height == 0) return fail(YART_ERR_INVALID, "width and height must be > 0");
+  std::lock_guard<std::mutex> lk(m->mu);
   const int n = m->n;
-  const uint32_t W = p->width, H = p->height;
-  const size_t pk_bytes = sizeof(double) * packet_len(W, H, (uint32_t)n);
-  const size_t frame_bytes = sizeof(double) * 3 * (size_t)W * H;
-  int old = 0;
-  (void)hipGetDevice(&old);
-  struct Restore { int d; ~Restore() { (void)hipSetDevice(d); } } restore{old};
-
-  std::vector<Progress> pr((size_t)n);
-  struct FreeAll { std::vector<Progress>& v; ~FreeAll() { for (auto& p : v) free_progress(p); } } free_all{pr};
-  std::vector<hipEvent_t> t0((size_t)n), t1((size_t)n), done((size_t)n);
-  struct Events {
-    std::vector<hipEvent_t>* v[3];
-    ~Events() { for (auto* x : v) for (hipEvent_t e : *x) if (e) (void)hipEventDestroy(e); }
-  } events{{&t0, &t1, &done}};
-  hipEvent_t g1 = nullptr;
-
-  // 1. every device renders its shard, packed, on its own stream
-  for (int d = 0; d < n; ++d) {
-    HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
-    hipStream_t st = m->streams[(size_t)d];
-    if (m->packed_bytes[(size_t)d] < pk_bytes) {
-      if (m->packed[(size_t)d]) {
-        HIP_TRY(hipStreamSynchronize(st), "drain");
-        HIP_TRY(hipFree(m->packed[(size_t)d]), "hipFree");
-      }
-      m->packed[(size_t)d] = nullptr; m->packed_bytes[(size_t)d] = 0;
-      HIP_TRY(hipMalloc(&m->packed[(size_t)d], pk_bytes), "hipMalloc packed shard");
-      HIP_TRY(hipMemsetAsync(m->packed[(size_t)d], 0, pk_bytes, st), "hipMemset");
-      m->packed_bytes[(size_t)d] = pk_bytes;
+  const size_t frame_bytes = sizeof(double) * 3 * (size_t)p->width * p->height;
+  RestoreDevice restore;
+  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
+  hipStream_t hs = m->host_stream;
+  if (m->frame_bytes < frame_bytes) {
+    if (m->frame) {
+      HIP_TRY(hipStreamSynchronize(hs), "drain");
+      HIP_TRY(hipFree(m->frame), "hipFree");
     }
-    if (d == 0 && m->frame_bytes < frame_bytes) {
-      if (m->frame) {
-        HIP_TRY(hipStreamSynchronize(st), "drain");
-        HIP_TRY(hipFree(m->frame), "hipFree");
-      }
-      m->frame = nullptr; m->frame_bytes = 0;
-      HIP_TRY(hipMalloc(&m->frame, frame_bytes), "hipMalloc frame");
-      m->frame_bytes = frame_bytes;
-    }
-    HIP_TRY(hipEventCreate(&t0[(size_t)d]), "hipEventCreate");
-    HIP_TRY(hipEventCreate(&t1[(size_t)d]), "hipEventCreate");
-    HIP_TRY(hipEventCreateWithFlags(&done[(size_t)d], hipEventDisableTiming), "hipEventCreate");
-    RenderArgs a;
-    yart_render_params q = *p;
-    q.shard_index = (uint32_t)d;
-    q.shard_count = (uint32_t)n;
-    if (int rc = make_args(m->scenes[(size_t)d], cam, &q, m->packed[(size_t)d], a)) return rc;
-    a.packed = 1;
-    if (progress) {
-      if (int rc = alloc_progress(pr[(size_t)d])) return rc;
-      pr[(size_t)d].pixels = shard_pixels(W, H, (uint32_t)d, (uint32_t)n);
-    }
-    HIP_TRY(hipEventRecord(t0[(size_t)d], st), "hipEventRecord");
-    if (int rc = launch_frame(m->scenes[(size_t)d], a, p->samples_per_unit, false, st, progress ? &pr[(size_t)d] : nullptr))
-      return rc;
-    HIP_TRY(hipEventRecord(t1[(size_t)d], st), "hipEventRecord");
-    HIP_TRY(hipEventRecord(done[(size_t)d], st), "hipEventRecord");
+    m->frame = nullptr; m->frame_bytes = 0;
+    HIP_TRY(hipMalloc(&m->frame, frame_bytes), "hipMalloc frame");
+    m->frame_bytes = frame_bytes;
   }
-  // 2. progress on this thread while the devices render
-  std::vector<Progress*> pp;
+  std::vector<Progress> pr((size_t)(progress ? n : 0));
+  struct FreeAll { std::vector<Progress>& v; ~FreeAll() { for (auto& x : v) free_progress(x); } } free_all{pr};
   uint64_t total_px = 0;
-  for (auto& x : pr) { pp.push_back(&x); total_px += x.pixels; }
-  if (int rc = wait_with_progress(done, m->devices, pp, total_px, progress, user)) return rc;
-  // 3. ONE gather to devices[0] (one group over the single-process communicators), then unpack
-  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
-  if (int rc = ensure_recv(m->comms[0], pk_bytes * (size_t)n)) return rc;
-  NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
-  for (int d = 0; d < n; ++d) {
-    (void)hipSetDevice(m->devices[(size_t)d]);
-    yart_comm* c = m->comms[(size_t)d];
-    ncclResult_t r = ncclGather(m->packed[(size_t)d], d == 0 ? c->recv : nullptr, pk_bytes / sizeof(double), ncclFloat64, 0,
-                                c->comm, m->streams[(size_t)d]);
-    if (r != ncclSuccess) { (void)ncclGroupEnd(); return nccl_fail(r, "ncclGather"); }
-  }
-  NCCL_TRY(ncclGroupEnd(), "ncclGroupEnd");
-  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
-  hipStream_t st0 = m->streams[0];
-  HIP_TRY(launch_unpack_shards(m->comms[0]->recv, (uint32_t)n, pk_bytes / sizeof(double), W, H, m->frame, st0),
-          "launch k_unpack_shards");
-  HIP_TRY(hipEventCreate(&g1), "hipEventCreate");
-  std::unique_ptr<std::remove_pointer<hipEvent_t>::type, decltype(&hipEventDestroy)> hold(g1, &hipEventDestroy);
-  HIP_TRY(hipEventRecord(g1, st0), "hipEventRecord");
-  HIP_TRY(hipMemcpyAsync(xyz_sum_out, m->frame, frame_bytes, hipMemcpyDeviceToHost, st0), "copy frame");
-  HIP_TRY(hipStreamSynchronize(st0), "gather");
-  for (int d = 1; d < n; ++d) {
+  std::vector<Progress*> pp;
+  for (int d = 0; d < (int)pr.size(); ++d) {
     HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
-    HIP_TRY(hipStreamSynchronize(m->streams[(size_t)d]), "gather");
+    if (int rc = alloc_progress(pr[(size_t)d])) return rc;
+    pr[(size_t)d].pixels = shard_pixels(p->width, p->height, (uint32_t)d, (uint32_t)n);
+    total_px += pr[(size_t)d].pixels;
+    pp.push_back(&pr[(size_t)d]);
   }
-  // timing: slowest device's render; gather + unpack on the root after its render
-  double r = 0.0;
-  for (int d = 0; d < n; ++d) {
-    float ms = 0.0f;
-    HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
-    HIP_TRY(hipEventElapsedTime(&ms, t0[(size_t)d], t1[(size_t)d]), "hipEventElapsedTime");
-    if (ms > r) r = ms;
-  }
-  float gms = 0.0f;
+  // everything (renders, gather, unpack) is enqueued before the host waits
+  if (int rc = multi_submit(m, cam, p, m->frame, hs, progress ? &pr : nullptr)) return rc;
   HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
-  HIP_TRY(hipEventElapsedTime(&gms, t1[0], g1), "hipEventElapsedTime");
-  m->render_ms = r;
-  m->gather_ms = gms;
+  hipEvent_t done;
+  HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate");
+  std::unique_ptr<std::remove_pointer<hipEvent_t>::type, decltype(&hipEventDestroy)> hold(done, &hipEventDestroy);
+  HIP_TRY(hipEventRecord(done, hs), "hipEventRecord");
+  if (int rc = wait_with_progress({done}, {m->devices[0]}, pp, total_px, progress, user)) return rc;
+  HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
+  HIP_TRY(hipMemcpyAsync(xyz_sum_out, m->frame, frame_bytes, hipMemcpyDeviceToHost, hs), "copy frame");
+  HIP_TRY(hipStreamSynchronize(hs), "copy frame");
+  uint32_t frames = 0;
+  // the host stream's slot is idle now: the timing of its frame
+  double r = 0.0, g = 0.0;
+  if (int rc = multi_timing(m, m->slots[hs].get(), &r, &g, &frames)) return rc;
+  m->render_ms = frames ? r / frames : 0.0;
+  m->gather_ms = frames ? g / frames : 0.0;
   return ok();
 }
 
@@ -302,5 +467,14 @@ int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gathe
 }
 
 void yart_multi_destroy(yart_multi* m) { delete m; }
+
+int yart_unpack_shards_async(int device, const double* d_recv, uint32_t shards, uint64_t stride, uint32_t width,
+                             uint32_t height, double* d_frame, void* stream) {
+  if (!d_recv || !d_frame || shards == 0 || width == 0 || height == 0) return fail(YART_ERR_INVALID, "bad argument");
+  if (stride < packet_len(width, height, shards)) return fail(YART_ERR_INVALID, "stride below the largest shard's packet");
+  DeviceGuard g(device);
+  HIP_TRY(launch_unpack_shards(d_recv, shards, stride, width, height, d_frame, (hipStream_t)stream), "launch k_unpack_shards");
+  return ok();
+}
 
 }  // extern "C"

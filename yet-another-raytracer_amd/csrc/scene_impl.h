@@ -46,6 +46,7 @@ struct StreamState {
 struct Progress {
   uint32_t* host = nullptr;    // host view (hipHostMalloc, coherent)
   uint32_t* device = nullptr;  // the kernels' view of the same word
+  uint32_t* counter = nullptr; // device memory: finished units of the fused path (atomic)
   uint32_t total_units = 0;    // over all passes of the frame
   uint64_t pixels = 0;         // covered pixels of the shard
 };

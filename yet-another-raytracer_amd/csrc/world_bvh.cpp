@@ -90,9 +90,14 @@ double half_area(const double lo[3], const double hi[3]) {
 // is cheaper than a node visit plus the children's expected tests). A sphere of the random scene's
 // ground (radius 1000) gets a leaf near the root this way instead of widening every box on its
 // median-split path, which every ray then visited.
-size_t kMaxLeaf = 4;
-double kNodeCost = 0.7;  // one DevWorldNode visit (two f32 box tests) vs one primitive test
-size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const double nlo[3], const double nhi[3]) {
+// Per build (YART_WORLD_SAH is read once into the build's own copy: no shared state between
+// concurrent yart_scene_create calls).
+struct SahParams {
+  size_t max_leaf = 4;
+  double node_cost = 0.7;  // one DevWorldNode visit (two f32 box tests) vs one primitive test
+};
+size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const double nlo[3], const double nhi[3],
+                 const SahParams& prm) {
   const size_t n = end - begin;
   const double parent = half_area(nlo, nhi);
   double best = INFINITY;
@@ -116,7 +121,7 @@ size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const doubl
     }
   }
   if (best_axis < 0) return 0;
-  if (n <= kMaxLeaf && parent > 0.0 && (double)n * parent <= kNodeCost * parent + best) return 0;
+  if (n <= prm.max_leaf && parent > 0.0 && (double)n * parent <= prm.node_cost * parent + best) return 0;
   std::sort(items.begin() + begin, items.begin() + end, [best_axis](const Item& a, const Item& b) {
     return a.c[best_axis] < b.c[best_axis] || (a.c[best_axis] == b.c[best_axis] && a.idx < b.idx);
   });
@@ -124,7 +129,7 @@ size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const doubl
 }
 
 void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, uint32_t level, BuiltWorld& out,
-           bool sah) {
+           bool sah, const SahParams& prm) {
   out.depth = std::max(out.depth, level);
   DevWorldNode& n = out.nodes[node];
   set_box(n, items.data() + begin, end - begin);
@@ -135,7 +140,7 @@ void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, ui
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t i = begin; i < end; ++i)
       for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], items[i].lo[k]); hi[k] = std::max(hi[k], items[i].hi[k]); }
-    cut = sah_split(items, begin, end, lo, hi);
+    cut = sah_split(items, begin, end, lo, hi, prm);
     if (cut == 0) {  // a leaf
       n.count = (uint32_t)(end - begin);
       n.first = (uint32_t)out.objs.size();
@@ -173,8 +178,8 @@ void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, ui
   out.nodes.emplace_back();
   out.nodes[node].count = 0;
   out.nodes[node].first = left;
-  build(items, begin, mid, left, level + 1, out, sah);
-  build(items, mid, end, left + 1, level + 1, out, sah);
+  build(items, begin, mid, left, level + 1, out, sah, prm);
+  build(items, mid, end, left + 1, level + 1, out, sah, prm);
 }
 
 }  // namespace
@@ -189,14 +194,15 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     items[i].idx = (uint32_t)i;
   }
   // YART_WORLD_SAH=node_cost,max_leaf: tuning sweeps (tools/gpu_world.sh)
+  SahParams prm;
   if (const char* e = std::getenv("YART_WORLD_SAH")) {
     double c = 0.0;
     unsigned l = 0;
-    if (std::sscanf(e, "%lf,%u", &c, &l) == 2 && c > 0.0 && l >= 1) { kNodeCost = c; kMaxLeaf = l; }
+    if (std::sscanf(e, "%lf,%u", &c, &l) == 2 && c > 0.0 && l >= 1) { prm.node_cost = c; prm.max_leaf = l; }
   }
   out.nodes.reserve(2 * objs.size());
   out.nodes.emplace_back();
-  build(items, 0, items.size(), 0, 0, out, sah);
+  build(items, 0, items.size(), 0, 0, out, sah, prm);
   // the device walk pushes at most one entry per level into its kStackSlots-deep stack
   if (sah && out.depth >= (uint32_t)kStackSlots) return build_world_bvh(objs, out, false);
   return out.depth < (uint32_t)kStackSlots;

@@ -101,6 +101,9 @@ def load_device():
     _sig(L, "yart_gather_frame_async", I, P, P, U32, U32, I, P, P)
     _sig(L, "yart_multi_create", I, I, P, C.POINTER(abi.SceneDesc), C.POINTER(P))
     _sig(L, "yart_render_multi", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, abi.PROGRESS_FN, P)
+    _sig(L, "yart_render_multi_async", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, P)
+    _sig(L, "yart_multi_frame_timing", I, P, C.POINTER(D), C.POINTER(D), C.POINTER(U32))
+    _sig(L, "yart_unpack_shards_async", I, I, P, U32, U64, U32, U32, P, P)
     _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
     _sig(L, "yart_multi_destroy", None, P)
     _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
@@ -280,6 +283,13 @@ def shard_packed_len(width, height, shard_index, shard_count):
     return int(load_device().yart_shard_packed_len(width, height, shard_index, shard_count))
 
 
+def unpack_shards_async(device, d_recv_ptr, shards, stride, width, height, d_frame_ptr, stream_ptr):
+    """yart_unpack_shards_async: `shards` packed shards back to back (stride doubles apart) ->
+    the W x H x 3 frame, on the device."""
+    _check_dev(load_device().yart_unpack_shards_async(device, C.c_void_p(d_recv_ptr), shards, stride, width, height,
+                                                      C.c_void_p(d_frame_ptr), C.c_void_p(stream_ptr)))
+
+
 class Comm:
     """An RCCL communicator of libyart (yart_comm_init_rank): one rank per process/GPU. The root's
     128-byte id reaches the other ranks through the caller's own channel (e.g. torch.distributed)."""
@@ -332,6 +342,19 @@ class MultiScene:
         cb = abi.PROGRESS_FN((lambda px, user: progress(px)) if progress else 0)
         _check_dev(load_device().yart_render_multi(self._m, C.byref(cam), C.byref(params), _ptr(out), cb, None))
         return out
+
+    def render_async(self, cam, params, d_frame_ptr, stream_ptr):
+        """yart_render_multi_async: the frame lands in d_frame (on devices[0]) in the order of
+        stream_ptr (a stream of devices[0]); no host wait."""
+        _check_dev(load_device().yart_render_multi_async(self._m, C.byref(cam), C.byref(params), C.c_void_p(d_frame_ptr),
+                                                         C.c_void_p(stream_ptr)))
+
+    def frame_timing(self):
+        """(render_ms, gather_ms, frames) summed over the async frames since the last call: the
+        slowest device's render time and the root's gather + unpack time."""
+        r, g, n = C.c_double(), C.c_double(), C.c_uint32()
+        _check_dev(load_device().yart_multi_frame_timing(self._m, C.byref(r), C.byref(g), C.byref(n)))
+        return r.value, g.value, n.value
 
     def last_timing(self):
         r, g = C.c_double(), C.c_double()
