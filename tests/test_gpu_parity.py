@@ -403,6 +403,31 @@ def test_shards_partition_the_frame(dev):
     np.testing.assert_array_equal(parts[0] + parts[1] + parts[2], full)
 
 
+@pytest.mark.parametrize("scene,W,H,spp,depth", [("bunny", 40, 40, 4, 50), ("david", 48, 27, 2, 50), ("david", 24, 16, 3, 1),
+                                                 ("david", 16, 16, 2, 0)])
+def test_wavefront_and_megakernel_agree(dev, scene, W, H, spp, depth, monkeypatch):
+    """Mesh scenes render on the wavefront path (k_wf_shade / k_wf_trace) by default. It must give
+    the megakernel's bits (YART_MESH_WF=0) and the oracle's: with the default pool, with a 256-path
+    pool (hundreds of iterations, every path slot regenerated many times), and over several
+    scratch passes."""
+    p = yart.Preset(scene)
+    cam = p.camera(W, H)
+    prm = yart.render_params(W, H, spp, depth)
+    wf = yart.DeviceScene(p).render(cam, prm)
+    monkeypatch.setenv("YART_WF_POOL", "256")
+    small = yart.DeviceScene(p).render(cam, prm)
+    monkeypatch.setenv("YART_SCRATCH_BYTES", str(((W + 7) // 8) * ((H + 7) // 8) * 64 * 24))  # one sample per pass
+    passes = yart.DeviceScene(p).render(cam, prm)
+    monkeypatch.setenv("YART_MESH_WF", "0")
+    mega = yart.DeviceScene(p).render(cam, prm)
+    np.testing.assert_array_equal(wf, mega)
+    np.testing.assert_array_equal(small, mega)
+    np.testing.assert_array_equal(passes, mega)
+    if depth > 0:
+        np.testing.assert_array_equal(wf, O.OracleScene(p.desc).render(cam, prm, threads=0))
+    assert (wf[O.coverage(W, H)].sum(axis=-1) != 0).mean() > 0.05
+
+
 def test_finalize_matches_oracle(dev):
     p = yart.Preset("cornell-box")
     W, H, spp = 96, 64, 8

@@ -15,5 +15,5 @@ for line in sys.stdin:
     k, _, v = t.partition(":")
     if cur and k.strip() in ("VGPRs", "VGPRs Spill", "SGPRs Spill", "ScratchSize [bytes/lane]"): rows[cur][k.strip()] = v.strip()
 for n in sorted(rows):
-    if "k_render" in n: print(n.replace("_ZN8yart_dev8k_renderI", "k_render<").split("EEv")[0], rows[n])
+    if "k_render" in n or "k_wf" in n: print(n.replace("_ZN8yart_dev8k_renderI", "k_render<").split("EEv")[0], rows[n])
 '

@@ -150,7 +150,11 @@ uint32_t assign_lpf(std::vector<DevObject>& objs, std::vector<DevObject>& lights
 yart_scene::~yart_scene() {
   DeviceGuard g(device);
   for (void* p : owned) (void)hipFree(p);
-  for (auto& kv : streams) (void)hipFree(kv.second->scratch);
+  for (auto& kv : streams) {
+    (void)hipFree(kv.second->scratch);
+    if (kv.second->wf_mem) (void)hipFree(kv.second->wf_mem);
+    if (kv.second->wf_status_host) (void)hipHostFree(kv.second->wf_status_host);
+  }
   for (hipStream_t st : owned_streams) (void)hipStreamDestroy(st);
   for (auto& kv : frames)
     for (auto& f : kv.second)
@@ -342,6 +346,17 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   for (uint32_t i = 0; i < d->n_textures; ++i)
     ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE || d->textures[i].kind == YART_TEX_IMAGE;
 
+  // Mesh scenes render on the wavefront path (k_wf_shade / k_wf_trace) unless they need the EXT
+  // kernels (media, moving spheres, noise / image textures); YART_MESH_WF=0 keeps the megakernel.
+  {
+    const char* e = std::getenv("YART_MESH_WF");
+    s->wavefront = ds.has_mesh && !ds.has_ext && !(e && std::atoi(e) == 0);
+    if (const char* pe = std::getenv("YART_WF_POOL")) {
+      const long v = std::atol(pe);
+      if (v >= 256) s->wf_pool = (uint32_t)std::min<long>(v, 1l << 24) / 256u * 256u;
+    }
+  }
+
   yart_scene_info& in = s->info;
   in.device = device; in.n_objects = d->n_objects; in.n_lights = d->n_lights; in.n_meshes = d->n_meshes;
   in.bvh_nodes = nodes; in.bvh_leaves = leaves; in.bvh_max_depth = depth;
@@ -524,6 +539,101 @@ void push_frame(yart_scene* s, hipStream_t stream, std::vector<hipEvent_t>&& f) 
   frames.push_back(std::move(f));
 }
 
+// The wavefront buffers of a stream: two queues of `pool` paths (SoA, WfQueue), the 5 queue
+// counters (a ring of 4 + a zero word) and the host-mapped status ring. Called with frame_mu held.
+constexpr uint32_t kWfStatusRing = 64, kWfSentinel = 0xFFFFFFFFu;
+size_t wf_queue_bytes(uint32_t pool) { return (size_t)pool * (6 * 8 + 2 * 8 + 2 * 4 + 3 * 8 + 2 * 4); }
+int stream_wf(StreamState* st, hipStream_t stream, uint32_t pool, WfQueue q[2], uint32_t** counters) {
+  const size_t bytes = 2 * wf_queue_bytes(pool) + 256;
+  if (st->wf_bytes < bytes || st->wf_pool != pool) {
+    if (st->wf_mem) {
+      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its path queues");
+      HIP_TRY(hipFree(st->wf_mem), "hipFree path queues");
+    }
+    st->wf_mem = nullptr; st->wf_bytes = 0; st->wf_pool = 0;
+    HIP_TRY(hipMalloc(&st->wf_mem, bytes), "hipMalloc path queues");
+    st->wf_bytes = bytes; st->wf_pool = pool;
+  }
+  if (!st->wf_status_host) {
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, kWfStatusRing * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc status ring");
+    void* d = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) { (void)hipHostFree(h); return hip_fail(e, "hipHostGetDevicePointer"); }
+    st->wf_status_host = static_cast<uint32_t*>(h);
+    st->wf_status_dev = static_cast<uint32_t*>(d);
+  }
+  char* p = static_cast<char*>(st->wf_mem);
+  for (int b = 0; b < 2; ++b) {
+    auto take = [&](size_t n) { char* r = p; p += n; return r; };
+    q[b].o = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
+    q[b].d = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
+    q[b].T = reinterpret_cast<double*>(take(8 * (size_t)pool));
+    q[b].wl = reinterpret_cast<double*>(take(8 * (size_t)pool));
+    q[b].ht = reinterpret_cast<double*>(take(8 * (size_t)pool));
+    q[b].hu = reinterpret_cast<double*>(take(8 * (size_t)pool));
+    q[b].hv = reinterpret_cast<double*>(take(8 * (size_t)pool));
+    q[b].job = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+    q[b].depth = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+    q[b].hobj = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+    q[b].hsub = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+  }
+  *counters = reinterpret_cast<uint32_t*>(p);
+  return YART_OK;
+}
+
+// One pass on the wavefront path: shade/trace iterations until the pass's jobs are done. The
+// number of iterations is data-dependent, so the host keeps kWfLookahead iterations queued ahead
+// of the device and stops when an iteration reports an empty queue (the few iterations already
+// queued behind it find nothing to do). The stream must be idle-safe to query: a device fault
+// shows up as a stream error, never as a spin without end.
+constexpr uint32_t kWfLookahead = 6;
+int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t stream) {
+  const uint64_t total = (uint64_t)b.n_blocks * b.s_count * 64;
+  if (total == 0) return YART_OK;
+  if (total > 0xFFFFFF00ull) return fail(YART_ERR_INVALID, "wavefront pass over 2^32 jobs");
+  uint32_t pool = s->wf_pool;
+  if ((uint64_t)pool > (total + 255) / 256 * 256) pool = (uint32_t)((total + 255) / 256 * 256);
+  WfQueue q[2];
+  uint32_t* cnt = nullptr;
+  if (int rc = stream_wf(st, stream, pool, q, &cnt)) return rc;
+  HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), stream), "zero the queue counters");
+  volatile uint32_t* hs = st->wf_status_host;
+  WfArgs w;
+  w.jobs = cnt + 5;
+  w.total_jobs = (uint32_t)total;
+  w.pool = pool;
+  for (uint32_t k = 0;; ++k) {
+    if (k > (1u << 22)) return fail(YART_ERR_DEVICE, "wavefront pass did not finish");
+    __atomic_store_n(&hs[k % kWfStatusRing], kWfSentinel, __ATOMIC_RELAXED);
+    w.in = q[(k + 1) & 1u];
+    w.out = q[k & 1u];
+    w.n_in = k == 0 ? cnt + 4 : cnt + (k - 1) % 4;  // cnt[4] stays 0
+    w.n_out = cnt + k % 4;
+    w.n_next = cnt + (k + 1) % 4;
+    w.status = st->wf_status_dev + k % kWfStatusRing;
+    HIP_TRY(launch_wf_shade(s->dev, b, w, stream), "launch k_wf_shade");
+    HIP_TRY(launch_wf_trace(s->dev, b, w, stream), "launch k_wf_trace");
+    if (k < kWfLookahead) continue;
+    const uint32_t j = k - kWfLookahead;
+    uint32_t v;
+    for (int spin = 0;; ++spin) {
+      v = __atomic_load_n(&hs[j % kWfStatusRing], __ATOMIC_ACQUIRE);
+      if (v != kWfSentinel) break;
+      const hipError_t e = hipStreamQuery(stream);
+      if (e != hipErrorNotReady) {
+        v = __atomic_load_n(&hs[j % kWfStatusRing], __ATOMIC_ACQUIRE);
+        if (v != kWfSentinel) break;
+        return e != hipSuccess ? hip_fail(e, "wavefront iteration") : fail(YART_ERR_DEVICE, "wavefront iteration did not report");
+      }
+      if (spin > 8) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (v == 0) break;
+  }
+  return YART_OK;
+}
+
 }  // namespace
 
 namespace yart_impl {
@@ -534,6 +644,31 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
   if (prog) { a.progress = prog->device; a.progress_count = prog->counter; }
+  if (s->wavefront && !stats) {  // mesh scenes: the wavefront path, pass by pass over the scratch budget
+    double* scratch = nullptr;
+    const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
+    if (int rc = stream_scratch(st, stream, scratch_bytes + 256, &scratch)) return rc;
+    const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
+    if (int rc = take_events(s, 3 * (size_t)passes, ev)) return rc;
+    uint32_t k = 0;
+    for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp, ++k) {
+      RenderArgs b = a;
+      b.s_begin = s0;
+      b.s_count = a.spp - s0 < pl.pass_spp ? a.spp - s0 : pl.pass_spp;
+      b.chunk = b.s_count;
+      b.n_chunks = 1;
+      b.scratch = scratch;
+      b.n_units = b.n_blocks;
+      HIP_TRY(hipEventRecord(ev[3 * k], stream), "hipEventRecord");
+      if (int rc = wf_pass(s, st, b, stream)) return rc;
+      HIP_TRY(hipEventRecord(ev[3 * k + 1], stream), "hipEventRecord");
+      HIP_TRY(launch_accumulate(b, s0 == 0, stream), "launch k_accumulate");
+      HIP_TRY(hipEventRecord(ev[3 * k + 2], stream), "hipEventRecord");
+    }
+    if (prog) prog->total_units = 0;
+    push_frame(s, stream, std::move(ev));
+    return YART_OK;
+  }
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
     if (prog) prog->total_units = a.n_blocks;
     if (int rc = take_events(s, 2, ev)) return rc;

@@ -37,6 +37,37 @@ __host__ __device__ inline uint32_t shard_blocks(uint32_t total_blocks, uint32_t
   return total_blocks > shard_index ? (total_blocks - shard_index + shard_count - 1) / shard_count : 0u;
 }
 
+// Wavefront path for mesh scenes (k_wf_shade / k_wf_trace): the path state of up to `pool` paths
+// in HBM, double-buffered SoA (component-major: o[k * pool + i]), so the traversal kernel runs
+// with the registers of the walk alone. Queue q holds the paths that have a ray to trace; the
+// shade kernel reads queue q-1 (state + hits), writes queue q (state + new rays) compacted.
+struct WfQueue {
+  double* o;         // 3 * pool: ray origin (x block, y block, z block)
+  double* d;         // 3 * pool: ray direction
+  double* T;         // pool: throughput so far
+  double* wl;        // pool: the path's wavelength
+  uint32_t* job;     // pool: (local block, sample - s_begin, slot) as one index = the scratch slot
+  uint32_t* depth;   // pool: ray_reflectance's depth argument for the traced ray
+  double* ht;        // pool: closest hit t (k_wf_trace)
+  double* hu;        // pool: its u
+  double* hv;        // pool: its v
+  uint32_t* hobj;    // pool: world object hit, kWfMiss if none
+  uint32_t* hsub;    // pool: its box face / mesh triangle
+};
+constexpr uint32_t kWfMiss = 0xFFFFFFFFu;
+struct WfArgs {
+  WfQueue in, out;
+  const uint32_t* n_in;  // entries in `in` (device; a zero word for the first iteration)
+  uint32_t* n_out;       // entries appended to `out` (device, zeroed before the shade)
+  uint32_t* n_next;      // the counter the next iteration's shade appends to: k_wf_trace zeroes it
+  uint32_t* jobs;        // job counter of the pass (device)
+  uint32_t total_jobs;   // n_blocks * s_count * 64
+  uint32_t pool;
+  uint32_t* status;      // host-mapped: k_wf_trace stores the queue length it traced (0 = pass done)
+};
+hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream);
+hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream);
+
 hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream);
 // Adds a pass's per-sample values onto the per-pixel sums in sample order (first pass from 0).
 hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t stream);

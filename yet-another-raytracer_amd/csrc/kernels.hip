@@ -1785,6 +1785,132 @@ __device__ unsigned long long g_occ[32];
 #define OCC(k) do {} while (0)
 #endif
 
+// Material::scatter at the stored hit + the mixture pdf (material.rs, main.rs:548-584): the path's
+// next ray and throughput, or its end. One body for both math policies (the Fast cores first; a
+// lane whose operand left a core's range re-runs it on the IEEE sequences from the same inputs
+// and the same draws) and for both render paths (k_render's fused loop, k_wf_shade).
+template <bool EXT, bool STATS, bool LPF, class MP>
+__device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, const V3& hp, const V3& hn, uint32_t hmat,
+                                           double hu, double hv, int wbin, const Ray& ray, double T, uint32_t depth,
+                                           Stats& st, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_,
+                                           bool& term_, double& Tp_, double& cosv_, bool& pend_) {
+#ifdef YART_OCC
+  const uint32_t lane = __lane_id();
+#endif
+    T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false; pend_ = false;
+    const DevMaterial& m = S.materials[hmat];
+    const uint32_t kind = m.kind;
+    if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+      OCC(OCC_LAMB);
+      // the albedo is looked up where it is multiplied in: fetched here, it was held (and
+      // spilled) through the direction sampling and the light pdfs
+      auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
+      const Onb uvw = onb_from_w(hn, mp);
+      V3 dir;
+      double pdf_val;
+      if (S.n_lights == 0) {
+        (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
+        dir = local(uvw, random_cosine_direction(g, mp));
+        pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
+      } else {
+        if (gen_range(g, 0.0, 1.0) < 0.5) {
+          // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+          OCC(OCC_LAMB_LIGHT);
+          const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+          dir = light_random(S.lights[k], hp, g, mp);
+        } else {
+          OCC(OCC_LAMB_COS);
+          dir = local(uvw, random_cosine_direction(g, mp));
+        }
+        if (LPF && S.n_lpf != 0) {  // finished after the world pass (resolve)
+          pdf_val = 0.0;
+          cosv_ = cosine_value(uvw, dir, mp);
+          pend_ = true;
+        } else {
+          const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+          double sum = -0.0;
+          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
+          pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
+        }
+      }
+      if (pend_) {
+        const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+        const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+        Tp_ = (T * att()) * spdf;
+        o_ = hp;
+        d_ = dir;
+        depth_ = depth - 1;
+      } else if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+        R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+        term_ = true;
+      } else {
+        const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+        const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+        T_ = ((T * att()) * spdf) / pdf_val;
+        o_ = hp;
+        d_ = dir;
+        depth_ = depth - 1;
+      }
+    } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
+      const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
+      V3 p;
+      for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+        const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+        p = mk(px, py, pz);
+        if (!(len2(p) >= 1.0)) break;
+      }
+      T_ = T * att;
+      o_ = hp;
+      d_ = p;
+      depth_ = depth - 1;
+    } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+      OCC(OCC_METAL);
+      const V3 reflected = reflect(mp.unit(ray.d), hn);
+      V3 p;
+      for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+        const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+        p = mk(px, py, pz);
+        if (!(len2(p) >= 1.0)) break;
+      }
+      const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
+      T_ = T * att;
+      o_ = hp;
+      d_ = add(reflected, smul(m.fuzz, p));
+      depth_ = depth - 1;
+    } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+      OCC(OCC_DIEL);
+      const double wl2 = ray.wl * ray.wl;
+      const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+      const double n = mp.sqrt(n2);
+      // |d| divides the incidence cosine and, in unit_vector(d), the three components
+      const PosDen ld = mp.den(mp.len(ray.d));
+      V3 outward;
+      double ni_over_nt, cosine;
+      if (dot(ray.d, hn) > 0.0) {
+        outward = neg(hn); ni_over_nt = n; cosine = mp.quo(n * dot(ray.d, hn), ld);
+      } else {
+        outward = hn; ni_over_nt = 1.0 / n; cosine = mp.quo(-dot(ray.d, hn), ld);
+      }
+      const V3 uv = mk(mp.quo(ray.d.x, ld), mp.quo(ray.d.y, ld), mp.quo(ray.d.z, ld));  // refract (material.rs:195-205)
+      const double dt = dot(uv, outward);
+      const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+      V3 out;
+      if (disc > 0.0) {
+        const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, mp.sqrt(disc)));
+        double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+        r0 = r0 * r0;
+        const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+        out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
+      } else {
+        out = reflect(ray.d, hn);
+      }
+      T_ = T * 1.0;
+      o_ = hp;
+      d_ = out;
+      depth_ = depth - 1;
+    }
+}
+
 #ifndef YART_LPF
 #define YART_LPF 0
 #endif
@@ -1976,118 +2102,8 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
         auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
                            double& Tp_, double& cosv_, bool& pend_) {
-          T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false; pend_ = false;
-          const DevMaterial& m = S.materials[hmat];
-          const uint32_t kind = m.kind;
-          if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-            OCC(OCC_LAMB);
-            // the albedo is looked up where it is multiplied in: fetched here, it was held (and
-            // spilled) through the direction sampling and the light pdfs
-            auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
-            const Onb uvw = onb_from_w(hn, mp);
-            V3 dir;
-            double pdf_val;
-            if (S.n_lights == 0) {
-              (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
-              dir = local(uvw, random_cosine_direction(g, mp));
-              pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
-            } else {
-              if (gen_range(g, 0.0, 1.0) < 0.5) {
-                // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
-                OCC(OCC_LAMB_LIGHT);
-                const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
-                dir = light_random(S.lights[k], hp, g, mp);
-              } else {
-                OCC(OCC_LAMB_COS);
-                dir = local(uvw, random_cosine_direction(g, mp));
-              }
-              if (LPF && S.n_lpf != 0) {  // finished after the world pass (resolve)
-                pdf_val = 0.0;
-                cosv_ = cosine_value(uvw, dir, mp);
-                pend_ = true;
-              } else {
-                const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-                double sum = -0.0;
-                for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
-                pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
-              }
-            }
-            if (pend_) {
-              const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
-              const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-              Tp_ = (T * att()) * spdf;
-              o_ = hp;
-              d_ = dir;
-              depth_ = depth - 1;
-            } else if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-              R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-              term_ = true;
-            } else {
-              const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
-              const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-              T_ = ((T * att()) * spdf) / pdf_val;
-              o_ = hp;
-              d_ = dir;
-              depth_ = depth - 1;
-            }
-          } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
-            V3 p;
-            for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-              const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-              p = mk(px, py, pz);
-              if (!(len2(p) >= 1.0)) break;
-            }
-            T_ = T * att;
-            o_ = hp;
-            d_ = p;
-            depth_ = depth - 1;
-          } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
-            OCC(OCC_METAL);
-            const V3 reflected = reflect(mp.unit(ray.d), hn);
-            V3 p;
-            for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-              const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-              p = mk(px, py, pz);
-              if (!(len2(p) >= 1.0)) break;
-            }
-            const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
-            T_ = T * att;
-            o_ = hp;
-            d_ = add(reflected, smul(m.fuzz, p));
-            depth_ = depth - 1;
-          } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
-            OCC(OCC_DIEL);
-            const double wl2 = ray.wl * ray.wl;
-            const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-            const double n = mp.sqrt(n2);
-            // |d| divides the incidence cosine and, in unit_vector(d), the three components
-            const PosDen ld = mp.den(mp.len(ray.d));
-            V3 outward;
-            double ni_over_nt, cosine;
-            if (dot(ray.d, hn) > 0.0) {
-              outward = neg(hn); ni_over_nt = n; cosine = mp.quo(n * dot(ray.d, hn), ld);
-            } else {
-              outward = hn; ni_over_nt = 1.0 / n; cosine = mp.quo(-dot(ray.d, hn), ld);
-            }
-            const V3 uv = mk(mp.quo(ray.d.x, ld), mp.quo(ray.d.y, ld), mp.quo(ray.d.z, ld));  // refract (material.rs:195-205)
-            const double dt = dot(uv, outward);
-            const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
-            V3 out;
-            if (disc > 0.0) {
-              const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, mp.sqrt(disc)));
-              double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
-              r0 = r0 * r0;
-              const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
-              out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
-            } else {
-              out = reflect(ray.d, hn);
-            }
-            T_ = T * 1.0;
-            o_ = hp;
-            d_ = out;
-            depth_ = depth - 1;
-          }
+          scatter_at<EXT, STATS, LPF>(S, mp, g, hp, hn, hmat, hu, hv, wbin, ray, T, depth, st, T_, o_, d_, depth_, R_,
+                                      term_, Tp_, cosv_, pend_);
         };
         double nT, nR, nTp = 0.0, ncosv = 0.0;
         V3 no, nd;
@@ -2202,6 +2218,197 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   if (STATS) {
     for (int i = 0; i < kNumStats; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
+  }
+}
+
+// ------------------------------------------------------------- wavefront path (mesh scenes)
+// The megakernel's loop split at the world query. k_wf_shade does, for
+// every path of the pool, what k_render does around the query: the record of the hit the last
+// trace found, the material's scatter (or the path's end: background, emission, depth 0) and,
+// for a path that ended, the scratch store of its sample and the camera ray of the next job; the
+// paths that have a ray to trace are appended to the next queue with one atomic per wave (ballot
+// + mbcnt). k_wf_trace then walks the world for the queued rays alone — the cooperative QBVH walk
+// with nothing else live, so it runs without the megakernel's register spills. Every draw is keyed
+// by (pixel, sample, phase) and every sample has its own scratch slot, so the split changes the
+// order work is done in and nothing else: the sums are bitwise the megakernel's (k_accumulate adds
+// the samples in order).
+
+// job = (local block * s_count + sample - s_begin) * 64 + slot, which is also its scratch index
+__device__ __forceinline__ void wf_job(const RenderArgs& A, uint32_t job, uint32_t& pixel, uint32_t& smp, uint32_t& x,
+                                       uint32_t& y) {
+  const uint32_t slot = job & 63u, rest = job >> 6;
+  const uint32_t blk = rest / A.s_count, s = rest - blk * A.s_count;
+  const uint32_t b = A.shard_index + blk * A.shard_count;
+  x = (b % A.blocks_x) * 8u + (slot & 7u);
+  y = (b / A.blocks_x) * 8u + (slot >> 3);
+  pixel = y * A.width + x;
+  smp = A.s_begin + s;
+}
+// ray_color + sanitize_sample_xyz (main.rs:526-535, 448-459) into the sample's scratch slot
+__device__ __forceinline__ void wf_store_sample(const RenderArgs& A, uint32_t job, double wl, double R) {
+  double cx, cy, cz;
+  cie_xyz(wl, cx, cy, cz);
+  double sx = cx * R, sy = cy * R, sz = cz * R;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(sz)) {
+    sx = sy = sz = 0.0;
+  } else if (!(sy <= 0.0 || sy <= kMaxLum)) {
+    const double k = kMaxLum / sy;
+    sx = sx * k; sy = sy * k; sz = sz * k;
+  }
+  double* q = A.scratch + 3 * (size_t)job;
+  q[0] = sx; q[1] = sy; q[2] = sz;
+}
+
+__global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfArgs F) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_in = *F.n_in, P = F.pool;
+  const uint32_t W = A.width, H = A.height;
+  Stats st;
+  Rng g;
+  g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
+  Ray ray;
+  ray.time = 0.0;  // no MovingSphere on this path (EXT scenes keep the megakernel)
+  ray.wl = 0.0;
+  ray.o = mk(0.0, 0.0, 0.0); ray.d = ray.o;
+  double T = 0.0;
+  uint32_t job = 0, depth = 0;
+  bool has = false;  // a ray to trace next
+  if (i < n_in) {  // the path traced last iteration: its hit (main.rs:548-587)
+    job = F.in.job[i]; depth = F.in.depth[i]; T = F.in.T[i]; ray.wl = F.in.wl[i];
+    ray.o = mk(F.in.o[i], F.in.o[P + i], F.in.o[2 * (size_t)P + i]);
+    ray.d = mk(F.in.d[i], F.in.d[P + i], F.in.d[2 * (size_t)P + i]);
+    const int wbin = spectrum_bin(ray.wl);
+    const uint32_t obj = F.in.hobj[i];
+    double R = 0.0;
+    bool term = false;
+    if (obj == kWfMiss) {
+      R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
+      term = true;
+    } else {
+      HitId id;
+      id.t = F.in.ht[i]; id.u = F.in.hu[i]; id.v = F.in.hv[i]; id.obj = obj; id.sub = F.in.hsub[i];
+      Hit h;
+      hit_record<true, false>(S, ray, id, h);
+      const DevMaterial& m = S.materials[h.mat];
+      const uint32_t kind = m.kind;
+      if (kind == YART_MAT_LAMBERTIAN || kind == YART_MAT_METAL || kind == YART_MAT_DIELECTRIC) {
+        uint32_t pixel, smp, x, y;
+        wf_job(A, job, pixel, smp, x, y);
+        rng_phase<false>(g, pixel, smp, A.max_depth - depth + 1u);
+        double nT, nR, nTp = 0.0, ncosv = 0.0;
+        V3 no, nd;
+        uint32_t ndepth;
+        bool nterm, npend;
+        Ieee im;
+        scatter_at<false, false, false>(S, im, g, h.p, h.n, h.mat, 0.0, 0.0, wbin, ray, T, depth, st, nT, no, nd, ndepth, nR,
+                                        nterm, nTp, ncosv, npend);
+        if (nterm) {
+          R = nR;
+          term = true;
+        } else if (ndepth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
+          R = nT * 1.0;
+          term = true;
+        } else {
+          T = nT; ray.o = no; ray.d = nd; depth = ndepth;
+          has = true;
+        }
+      } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
+        double emitted = 0.0;
+        if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<false>(S, m.texture, wbin, h.p);
+        R = T * emitted;
+        term = true;
+      }
+    }
+    if (term) wf_store_sample(A, job, ray.wl, R);
+  }
+  // A slot without a ray (its path ended, or none yet) starts the pass's next job: consecutive job
+  // ids to the asking lanes of the wave (one atomic per round), skipping pixels outside the crop
+  // grid (main.rs:636-647) and samples that end at once (max_depth 0).
+  bool need = !has && i < P;
+  if (*(volatile uint32_t*)F.jobs >= F.total_jobs) need = false;
+  for (;;) {
+    const uint64_t m = __ballot(need);
+    if (m == 0) break;
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(F.jobs, (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+    if (base >= F.total_jobs) break;
+    if (need) {
+      const uint32_t jb = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (jb >= F.total_jobs) {
+        need = false;
+      } else {
+        uint32_t pixel, smp, x, y;
+        wf_job(A, jb, pixel, smp, x, y);
+        if (x < W && y < H && covered(x, W) && covered(y, H)) {  // main.rs:692-698
+          job = jb;
+          rng_phase<false>(g, pixel, smp, 0u);
+          const double tx = (double)x + gen_f64(g);
+          const double u = tx / (double)(W - 1);
+          const double ty = (double)y + gen_f64(g);
+          const double v = 1.0 - ty / (double)(H - 1);
+          const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
+          ray = camera_ray(*kernarg_camera(), u, v, wl, g, false);
+          ray.time = 0.0;
+          T = 1.0;
+          depth = A.max_depth;
+          if (depth == 0) {
+            wf_store_sample(A, job, ray.wl, T * 1.0);
+          } else {
+            has = true;
+            need = false;
+          }
+        }
+      }
+    }
+  }
+  // the paths with a ray, compacted into the next queue
+  const uint64_t hm = __ballot(has);
+  if (hm) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(hm);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(F.n_out, (uint32_t)__popcll(hm));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+    if (has) {
+      const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+      F.out.o[k] = ray.o.x; F.out.o[P + k] = ray.o.y; F.out.o[2 * (size_t)P + k] = ray.o.z;
+      F.out.d[k] = ray.d.x; F.out.d[P + k] = ray.d.y; F.out.d[2 * (size_t)P + k] = ray.d.z;
+      F.out.T[k] = T; F.out.wl[k] = ray.wl; F.out.job[k] = job; F.out.depth[k] = depth;
+    }
+  }
+}
+
+#ifndef YART_WF_TRACE_WAVES
+#define YART_WF_TRACE_WAVES 4  // LDS-bound: the cooperative walk's 9.2 KB per wave
+#endif
+__global__ __launch_bounds__(256, YART_WF_TRACE_WAVES) void k_wf_trace(DevScene S, RenderArgs A, WfArgs F) {
+  __shared__ uint32_t s_stack[4 * kWaveLdsWords];
+  const uint32_t n = *F.n_out, P = F.pool;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *F.n_next = 0u;  // the next iteration's queue counter (nothing reads it any more)
+    __hip_atomic_store(F.status, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (blockIdx.x * 256u >= n) return;  // workgroup-uniform: the walk needs whole waves
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool want = i < n;
+  const uint32_t k = want ? i : 0u;
+  Ray r;
+  r.o = mk(F.out.o[k], F.out.o[P + k], F.out.o[2 * (size_t)P + k]);
+  r.d = mk(F.out.d[k], F.out.d[P + k], F.out.d[2 * (size_t)P + k]);
+  r.time = 0.0; r.wl = 0.0;
+  HitId id;
+  Stats st;
+  const QueryCtx q{0u, 0u, 0u, 0u, 0u};  // no media on this path
+  uint32_t* stk = &s_stack[wave * kWaveLdsWords + lane];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kWaveLdsWords]);
+  const bool hit = world_closest<true, false, false>(S, want, r, 0.001, INFINITY, id, stk, coop, st, q);
+  if (want) {
+    F.out.ht[i] = id.t; F.out.hu[i] = id.u; F.out.hv[i] = id.v;
+    F.out.hobj[i] = hit ? id.obj : kWfMiss;
+    F.out.hsub[i] = id.sub;
   }
 }
 
@@ -2379,6 +2586,14 @@ hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hip
     if (s.has_ext) YART_LAUNCH(false, false, true); else YART_LAUNCH(false, false, false);
   }
 #undef YART_LAUNCH
+  return hipGetLastError();
+}
+hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
+  hipLaunchKernelGGL(k_wf_shade, dim3(w.pool / 256), dim3(256), 0, stream, s, a, w);
+  return hipGetLastError();
+}
+hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
+  hipLaunchKernelGGL(k_wf_trace, dim3(w.pool / 256), dim3(256), 0, stream, s, a, w);
   return hipGetLastError();
 }
 hipError_t launch_unpack_shards(const double* recv, uint32_t shards, size_t stride, uint32_t w, uint32_t h, double* frame,

@@ -14,6 +14,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <system_error>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -252,8 +254,10 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   RestoreDevice restore;
   MultiSlot* S = nullptr;
   if (int rc = multi_slot(m, caller, &S)) return rc;
-  // 1. renders, one per device, each straight into its packed shard
-  for (int d = 0; d < n; ++d) {
+  // 1. renders, one per device, each straight into its packed shard. A wavefront (mesh) frame keeps
+  // the host in its launch loop until the frame's last iterations are queued, so those devices are
+  // driven from a host thread each, all at once.
+  auto render_one = [&](int d) -> int {
     const size_t di = (size_t)d;
     HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
     hipStream_t st = S->streams[di];
@@ -275,7 +279,29 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
     if (int rc = make_args(m->scenes[di], cam, &q, S->packed[di], a)) return rc;
     a.packed = 1;
     Progress* pr = prog ? &(*prog)[di] : nullptr;
-    if (int rc = launch_frame(m->scenes[di], a, p->samples_per_unit, false, st, pr)) return rc;
+    return launch_frame(m->scenes[di], a, p->samples_per_unit, false, st, pr);
+  };
+  if (n > 1 && m->scenes[0]->wavefront) {
+    std::vector<int> rcs((size_t)n, YART_OK);
+    std::vector<std::string> errs((size_t)n);
+    std::vector<std::thread> th;
+    std::vector<int> here;
+    for (int d = 1; d < n; ++d) {
+      try {
+        th.emplace_back([&, d] { rcs[(size_t)d] = render_one(d); errs[(size_t)d] = yart_last_error(); });
+      } catch (const std::system_error&) {
+        here.push_back(d);
+      }
+    }
+    rcs[0] = render_one(0);
+    errs[0] = yart_last_error();
+    for (int d : here) { rcs[(size_t)d] = render_one(d); errs[(size_t)d] = yart_last_error(); }
+    for (auto& t : th) t.join();
+    for (int d = 0; d < n; ++d)
+      if (rcs[(size_t)d] != YART_OK) return fail(rcs[(size_t)d], errs[(size_t)d]);  // the message was thread-local
+  } else {
+    for (int d = 0; d < n; ++d)
+      if (int rc = render_one(d)) return rc;
   }
   // 2. the root's receive buffer (per slot: a later slot's gather may land while this one unpacks)
   HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");

@@ -38,6 +38,13 @@ struct StreamState {
   std::mutex frame_mu;
   double* scratch = nullptr;  // per-sample XYZ of the chunked path + the unit counter at its end
   size_t bytes = 0;
+  // wavefront path (mesh scenes): two path queues of `wf_pool` slots, the queue counters and the
+  // host-mapped status ring the iterations report into
+  void* wf_mem = nullptr;
+  size_t wf_bytes = 0;
+  uint32_t wf_pool = 0;
+  uint32_t* wf_status_host = nullptr;
+  uint32_t* wf_status_dev = nullptr;
 };
 
 // Progress of one frame (yart_render's callback): the kernels store `base + units handed out` to
@@ -56,6 +63,8 @@ struct Progress {
 struct yart_scene {
   int device = 0;
   int cu_count = 256;
+  bool wavefront = false;  // mesh scene without EXT features: k_wf_shade / k_wf_trace (YART_MESH_WF=0: megakernel)
+  uint32_t wf_pool = 1u << 20;  // paths in flight (YART_WF_POOL)
   yart_dev::DevScene dev{};
   std::vector<void*> owned;
   yart_scene_info info{};
