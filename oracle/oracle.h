@@ -52,6 +52,13 @@ int oracle_intersect(const oracle_scene* s, const double* rays, uint32_t n, doub
 /* Per-pixel 8x8-job coverage of main.rs:636-647 (1 = sampled). */
 int oracle_coverage(uint32_t w, uint32_t h, uint8_t* mask);
 
+/* An OBJ reader of the oracle's own (oracle_obj.c): TriangleMesh::from_obj (triangle.rs:111-174)
+ * over tobj's GPU_LOAD_OPTIONS, independent of the product's loader. positions n*9 f32, normals n*9
+ * and uvs n*6 (may be NULL) f64. 0 or a negative error (-4: a file mixing vertices with and
+ * without vn / vt, -5: unreadable). */
+int oracle_obj_count(const char* path, uint32_t* n_triangles);
+int oracle_obj_load(const char* path, float* positions, double* normals, double* uvs, uint32_t n_triangles);
+
 /* Restated unit pieces for known-answer tests. */
 void oracle_sanitize_sample_xyz(const double in[3], double out[3]);       /* main.rs:448-459 */
 uint8_t oracle_clamp_display_channel(double c);                          /* main.rs:461-463 */

@@ -47,6 +47,8 @@ def lib():
         "oracle_texture_probe": (D, [P, U32, D, P, D, D]),
         "oracle_acos": (D, [D]),
         "oracle_atan2": (D, [D, D]),
+        "oracle_obj_count": (I, [C.c_char_p, C.POINTER(U32)]),
+        "oracle_obj_load": (I, [C.c_char_p, P, P, P, U32]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -95,6 +97,21 @@ class OracleScene:
         obj = np.empty(n, dtype=np.int32)
         assert lib().oracle_intersect(self._s, _p(rays), n, _p(hits), _p(obj)) == 0
         return hits, obj
+
+
+def load_obj(path):
+    """The oracle's own OBJ reader (oracle_obj.c): positions (n, 9) f32, normals (n, 9) and uvs
+    (n, 6) f64."""
+    L = lib()
+    n = C.c_uint32()
+    rc = L.oracle_obj_count(str(path).encode(), C.byref(n))
+    assert rc == 0, rc
+    pos = np.zeros((n.value, 9), np.float32)
+    nrm = np.zeros((n.value, 9), np.float64)
+    uv = np.zeros((n.value, 6), np.float64)
+    rc = L.oracle_obj_load(str(path).encode(), _p(pos), _p(nrm), _p(uv), n.value)
+    assert rc == 0, rc
+    return pos, nrm, uv
 
 
 def finalize(xyz_sum, spp):

@@ -72,14 +72,20 @@ def test_philox_and_independent_chacha_streams_agree(scene, W, H, spp, depth):
 
 
 @pytest.mark.gpu
-def test_gpu_render_agrees_with_independent_chacha_streams():
-    """The HIP path (Philox) against the oracle's ChaCha12 streams, cornell box."""
-    p = yart.Preset("cornell-box")
-    W, H, spp = 32, 32, 64
+@pytest.mark.parametrize("scene,W,H,spp", [("cornell-box", 32, 32, 64), ("random-scene", 32, 24, 32),
+                                           ("bunny", 24, 24, 32), ("david", 32, 18, 32)])
+def test_gpu_render_agrees_with_independent_chacha_streams(scene, W, H, spp):
+    """The HIP path (Philox) against the oracle's ChaCha12 streams drawn in the reference's order
+    (main.rs:692-697, camera.rs:25-33, material.rs:276,311, pdf.rs:16-17,92, hittable.rs:119):
+    the cornell box, the random scene (metal fuzz, dispersive glass, negative albedos) and the two
+    mesh scenes - the bunny stand-in's SF66 glass and the david pair, white and glass (the mesh
+    scenes on the wavefront path)."""
+    p = yart.Preset(scene)
     cam = p.camera(W, H)
     dev = yart.DeviceScene(p.desc)
     s = O.OracleScene(p.desc)
     gpu = _stack(lambda seed: dev.render(cam, yart.render_params(W, H, spp, 50, seed=seed)), range(1, K + 1))
     chacha = _stack(lambda seed: s.render(cam, yart.render_params(W, H, spp, 50, seed=seed), chacha=True),
                     range(101, 101 + K))
+    assert not np.array_equal(gpu[0], chacha[0])
     _check(*_z_tests(gpu, chacha, spp))

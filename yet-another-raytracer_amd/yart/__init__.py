@@ -242,9 +242,9 @@ class DeviceScene:
 QBVH_TIES_DESC, QBVH_SERIAL = 1, 2
 
 
-def load_obj(path):
+def load_obj(path, with_uv=False):
     """TriangleMesh::from_obj's triangles (tobj semantics, libyart_host): f32 positions (n, 9) and
-    f64 normals (n, 9)."""
+    f64 normals (n, 9) (and f64 uvs (n, 6) with with_uv)."""
     H = load_host()
     n = C.c_uint32()
     _check_host(H.yart_obj_triangle_count(str(path).encode(), C.byref(n)))
@@ -252,7 +252,7 @@ def load_obj(path):
     nrm = np.zeros((n.value, 9), np.float64)
     uv = np.zeros((n.value, 6), np.float64)
     _check_host(H.yart_obj_load(str(path).encode(), _ptr(pos), _ptr(nrm), _ptr(uv), n.value))
-    return pos, nrm
+    return (pos, nrm, uv) if with_uv else (pos, nrm)
 
 
 def qbvh_build(positions, normals, flags=0):
