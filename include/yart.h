@@ -215,6 +215,8 @@ typedef struct yart_scene_info {
   uint32_t bvh_tied_leaves; /* leaves whose triangle order rests on equal keys              */
   double bvh_build_ms;    /* host QBVH build time, all meshes                           */
   double upload_ms;       /* host -> device copies of the scene                         */
+  uint32_t walk_nodes;    /* nodes of the front-to-back walk's SAH tree (0 = none)      */
+  uint32_t walk_depth;    /* its deepest root-to-leaf path in inner nodes               */
 } yart_scene_info;
 
 /* Per-launch work counters (optional, for roofline accounting; they slow the kernel). */

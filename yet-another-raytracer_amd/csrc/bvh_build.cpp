@@ -160,6 +160,9 @@ struct Builder {
       float* rec = &out->leaves[kTriFloats * (size_t)(off + i)];
       for (int c = 0; c < 9; ++c) rec[c] = v[c];
       std::memcpy(&rec[9], &li, 4);  // the leaf's index (LeafAux)
+      const uint32_t lane = i, tri = off + i;  // lane in the leaf, sorted index (the walk tree's records
+      std::memcpy(&rec[10], &lane, 4);        // carry the same three words, kernels.hip qbvh_coop)
+      std::memcpy(&rec[11], &tri, 4);
       const double* nn = &normals[9 * (size_t)perm[off + i]];
       for (int c = 0; c < 9; ++c) out->normals[9 * (size_t)(off + i) + c] = nn[c];
     }
@@ -317,6 +320,8 @@ static bool build_qbvh_impl(uint32_t n, const float* positions, const double* no
   rank_leaves(out, (uint32_t)out.nodes.size() - 1);
   out.tied_cuts = b.tied_cuts.load();
   out.tied_leaves = b.tied_leaves.load();
+  out.ref_nodes = (uint32_t)out.nodes.size();
+  out.walk_root = out.ref_nodes - 1;
   out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (3 * out.depth + 1 > (uint32_t)kMaxStackSlots) {  // the reference's 64-entry stack overflows too
     err = "QBVH too deep for the 64-entry traversal stack (depth " + std::to_string(out.depth) + ", qbvh.rs:382-384)";

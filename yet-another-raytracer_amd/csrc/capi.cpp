@@ -241,7 +241,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   double bg[kBins];
   for (int b = 0; b < kBins; ++b) bg[b] = spectrum_bin(d->background, b);
   std::vector<BuiltMesh> built(d->n_meshes);
-  uint32_t nodes = 0, leaves = 0, depth = 0, tied_cuts = 0, tied_leaves = 0;
+  uint32_t nodes = 0, leaves = 0, depth = 0, tied_cuts = 0, tied_leaves = 0, walk_nodes = 0, walk_depth = 0;
   double build_ms = 0.0;
   QbvhOptions qopt;  // YART_QBVH_TIES=desc: the tie-order probe (tests); YART_QBVH_THREADS=n
   if (const char* e = std::getenv("YART_QBVH_TIES")) qopt.ties_desc = std::strcmp(e, "desc") == 0;
@@ -251,10 +251,19 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     if (!ym.positions || !ym.normals) return fail(YART_ERR_INVALID, "mesh without positions/normals");
     std::string err;
     if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err, qopt)) return fail(YART_ERR_UNSUPPORTED, err);
+    // the front-to-back walk's own tree (walk_tree.cpp); YART_WALK_TREE=0 walks the reference tree
+    // front to back instead. Depth bound: the stack the walk gets (32 slots, 64 for deep meshes).
+    const char* wt = std::getenv("YART_WALK_TREE");
+    if (!(wt && std::atoi(wt) == 0)) {
+      const uint32_t slots = 3 * built[m].depth + 1 > (uint32_t)kStackSlots ? (uint32_t)kMaxStackSlots : (uint32_t)kStackSlots;
+      build_walk_tree(built[m], (slots - 1) / 3);
+    }
+    walk_nodes += built[m].walk_nodes;
+    walk_depth = std::max(walk_depth, built[m].walk_depth);
     tied_cuts += built[m].tied_cuts;
     tied_leaves += built[m].tied_leaves;
-    build_ms += built[m].build_ms;
-    nodes += (uint32_t)built[m].nodes.size();
+    build_ms += built[m].build_ms + built[m].walk_build_ms;
+    nodes += built[m].ref_nodes;
     leaves += (uint32_t)built[m].aux.size();
     depth = std::max(depth, built[m].depth);
   }
@@ -322,9 +331,12 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     const char* walk = std::getenv("YART_MESH_WALK");
     if (!(walk && std::strcmp(walk, "ref") == 0))
       HIP_TRY(upload(s->owned, b.aux.data(), b.aux.size(), &dm[m].aux, bytes), "upload leaf records");
-    dm[m].root = (uint32_t)b.nodes.size() - 1;
+    dm[m].root = b.ref_nodes - 1;
     dm[m].n_nodes = (uint32_t)b.nodes.size();
     dm[m].extent = b.extent;
+    dm[m].wroot = b.walk_root;
+    dm[m].n_recs = (uint32_t)(b.leaves.size() / kTriFloats);
+    dm[m].n_leaves = (uint32_t)b.aux.size();
   }
   HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
   if (use_world) {
@@ -376,6 +388,8 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   in.bvh_tied_cuts = tied_cuts;
   in.bvh_tied_leaves = tied_leaves;
   in.bvh_build_ms = build_ms;
+  in.walk_nodes = walk_nodes;
+  in.walk_depth = walk_depth;
   in.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - up0).count();
   *out = s.release();
   return ok();

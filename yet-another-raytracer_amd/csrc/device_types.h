@@ -67,10 +67,12 @@ struct alignas(16) DevNode {
   float hi[4][4];  // [k][2]: inner: node index; leaf: 1<<31 | count<<27 | leaf index; [k][3]: ranks
 };
 static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
-// Triangle records, 12 floats (48 B, three float4s) each, in the builder's sorted order: v0 v1 v2
-// (x y z each), the index of the leaf holding it (LeafAux), 2 pad. A leaf is the run
-// [first, first + count) its node id names (1<<31 | count<<27 | first); lane k of a quad reads
-// record first + k, and first + k is also the row of the normal table.
+// Triangle records, 12 floats (48 B, three float4s) each: v0 v1 v2 (x y z each), then three words —
+// the reference leaf holding the triangle (LeafAux index), its lane in that leaf and its sorted
+// index (the row of the normal table). The first n records are the reference tree's, in the
+// builder's sorted order; the next n the same triangles in the walk tree's leaf order
+// (walk_tree.cpp). A leaf is the run [first, first + count) its node id names
+// (1<<31 | count<<27 | first); lane k of a quad reads record first + k.
 constexpr int kTriFloats = 12;
 
 // Per-leaf side record for the front-to-back walk (qbvh_coop): the leaf's box exactly as its
@@ -87,13 +89,16 @@ static_assert(sizeof(LeafAux) == 64, "LeafAux must be 64 B");
 
 struct DevMesh {
   const DevNode* nodes;
-  const float* leaves;        // kTriFloats per sorted triangle (see DevNode)
+  const float* leaves;        // kTriFloats per triangle: sorted order, then the walk tree's leaf order
   const double* normals;      // 9 per sorted triangle: n0 n1 n2 (null when normals32 holds them)
   const float* normals32;     // the same in f32 when every value is exactly an f32 (OBJ vn)
   const LeafAux* aux;         // per leaf; null = walk in the reference's order only
   uint32_t root;              // the last node pushed (qbvh.rs:384)
-  uint32_t n_nodes;
+  uint32_t n_nodes;           // reference + walk tree nodes
   float extent;               // max |vertex coordinate| (error scale of the f32 box test)
+  uint32_t wroot;             // the walk tree's root (front to back; = root without a walk tree)
+  uint32_t n_recs;            // triangle records (sorted + walk order)
+  uint32_t n_leaves;          // reference leaves (LeafAux records)
 };
 
 // World BVH over the object list (not in the reference, whose HittableList is a linear scan):

@@ -976,6 +976,13 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 #define YART_COOP_ATTR __forceinline__  // inlined: +4% david, +11% bunny over a call (caller spills)
 #endif
 enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // per wave: lane 0 counts
+#ifdef YART_WALK_CHECK
+// Bounds-checked build of the cooperative walk (tools: make variant DEFS=-DYART_WALK_CHECK): every
+// record / node / stack index is checked before use; a violation sets a bit here (1 leaf record
+// range, 2 reference leaf index, 4 node index, 8 stack slot) and the access is skipped.
+__device__ unsigned int g_walk_fault;
+__device__ __forceinline__ void walk_fault(unsigned int bit) { atomicOr(&g_walk_fault, bit); }
+#endif
 template <bool STATS, int SLOTS = kCoopSlots>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
@@ -1001,7 +1008,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
   const __attribute__((address_space(1))) LeafAux* aux = (const __attribute__((address_space(1))) LeafAux*)M.aux;
-  const uint32_t root = M.root;
+  const uint32_t root = M.root, wroot = M.wroot;  // reference tree / walk tree (front to back)
   const float extent = M.extent;
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
@@ -1011,11 +1018,12 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   float inv32[3], tmin32 = 0.0f, teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
-  uint32_t pos = 0, node = 0, bleaf = 0;
+  uint32_t pos = 0, node = 0, bleaf = 0, bkey = 0;
   int cursor = 0;
   bool fnd = false, f2b = false;
   auto restart = [&](bool front_to_back) {
-    node = root;
+    node = front_to_back ? wroot : root;
+    bkey = 0xFFFFFFFFu;
     cursor = 0;
     fnd = false;
     tb = tin;    // best so far (reference order: the running t_max)
@@ -1071,34 +1079,46 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
       bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
-        const uint32_t count = (node >> 27) & 0xFu, first = node & ((1u << 27) - 1u);
+        uint32_t count = (node >> 27) & 0xFu;
+        const uint32_t first = node & ((1u << 27) - 1u);
+#ifdef YART_WALK_CHECK
+        if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
+#endif
         double t = INFINITY, u = 0.0, v = 0.0;
-        uint32_t key = 4u, id = 0u, li = 0u;
+        // A candidate's key orders equal t's as the reference visits them: front to back (either
+        // tree) by (the reference leaf's depth-first rank for this octant, lane in that leaf) and
+        // the quad lane in the low bits; in the reference's own order the lower lane of the leaf.
+        uint32_t key = 0xFFFFFFFFu, id = 0u, li = 0u;
         if (c < count) {
           const gfloat4p R = leaves + 3 * (size_t)(first + c);
           float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
           // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
           asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
-                       "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y));
+                       "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
+          li = __float_as_uint(p2.y);  // the record's reference leaf
+#ifdef YART_WALK_CHECK
+          if (li >= M.n_leaves) { walk_fault(2u); li = 0u; }
+#endif
           double tt, uu, vv;
           // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
-          // back: the tie goes to the reference's visiting order below)
+          // back: the tie goes to the reference's visiting order)
           if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tin, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
-            t = tt; u = uu; v = vv; key = c; id = first + c;
+            t = tt; u = uu; v = vv;
+            id = __float_as_uint(p2.w);  // sorted index: the normal table's row
+            key = f2b ? (aux[li].rank[pos] << 4) | (__float_as_uint(p2.z) << 2) | c : c;
           }
-          li = __float_as_uint(p2.y);
         }
-        li = quad_perm<0x00>(li);  // the leaf's index, from lane 0's record (count >= 1)
         if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
         quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
         quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
-        if (key < 4u) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
-          // t == tb only front to back with a best already held (t < t_max_in): the leaf the
-          // reference visits first keeps it (different leaves; in one leaf the lower lane won above)
-          const bool better = t < tb || aux[li].rank[pos] < aux[bleaf].rank[pos];
+        if (key != 0xFFFFFFFFu) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
+          const uint32_t w = key & 3u;
+          // t == tb only front to back with a best already held: the reference's order decides
+          const bool better = t < tb || key < bkey;
+          li = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane & ~3u) | w) << 2), (int)li);  // the winner's leaf
           if (better) {
-            tb = t; fnd = true; bleaf = li;
-            if (c == key) {
+            tb = t; fnd = true; bleaf = li; bkey = key;
+            if (c == w) {
               CoopRay& s = rays[ray];
               s.o[0] = t; s.o[1] = u; s.o[2] = v;
               s.d[0] = __longlong_as_double((long long)((1ull << 32) | id));
@@ -1114,6 +1134,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           }
         }
       } else {
+#ifdef YART_WALK_CHECK
+        if (node >= M.n_nodes) { walk_fault(4u); node = root; }
+#endif
         const gfloat4p N = nodes + 8 * (size_t)node;
         const float4 lo = ld4(N, c);
         float4 hi = ld4(N, 4 + c);
@@ -1146,10 +1169,19 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           nx |= quad_perm<0x4E>(nx);
           if (hk && rk != last) {
             const int slot = (cursor + (int)__popc(ordered & ((1u << rk) - 1u))) * 16 + (int)q;
-            qstk[slot] = child;
-            qent[slot] = ent;
+#ifdef YART_WALK_CHECK
+            if (slot >= SLOTS * 16) walk_fault(8u);
+            else
+#endif
+            {
+              qstk[slot] = child;
+              qent[slot] = ent;
+            }
           }
           cursor += (int)__popc(ordered) - 1;
+#ifdef YART_WALK_CHECK
+          if (cursor >= SLOTS) cursor = SLOTS - 1;
+#endif
           node = nx;
           popped = true;
         }
@@ -2721,5 +2753,14 @@ extern "C" int yart_debug_occupancy(int device, unsigned long long* out32) {
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(yart_dev::g_occ), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
   unsigned long long z[32] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_occ), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef YART_WALK_CHECK
+extern "C" int yart_debug_walk_fault(int device, unsigned int* out) {  // reads and clears the fault bits
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(yart_dev::g_walk_fault), sizeof(unsigned int)) != hipSuccess) return -1;
+  const unsigned int z = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_walk_fault), &z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -1,0 +1,208 @@
+// walk_tree.cpp — the front-to-back walk's own 4-wide tree over a mesh's triangles (not in the
+// reference). The reference's L4QBVH splits at the median triangle count (qbvh.rs:637-693), so a
+// node's children often overlap and a ray walks into boxes that a better-shaped tree would skip.
+// The walk tree regroups the same triangles by the surface-area heuristic; the answer stays the
+// reference tree's because the walk only proposes a candidate, keyed by the reference's order, and
+// the exact check at the end of each walk uses the reference leaf's box (kernels.hip, qbvh_coop).
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "bvh_build.h"
+
+namespace yart_dev {
+namespace {
+
+struct WItem {
+  float lo[3], hi[3];  // the triangle's box (exact f32: min/max of its vertices)
+  float c[3];          // centroid key (box centre), for binning only
+  uint32_t tri;        // sorted (reference) index
+};
+
+struct Box3 {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const WItem& t) {
+    for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], t.lo[k]); hi[k] = std::max(hi[k], t.hi[k]); }
+  }
+  void grow(const Box3& b) {
+    for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+  }
+  double area() const {
+    if (!(hi[0] >= lo[0])) return 0.0;
+    const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+    return x * y + y * z + z * x;
+  }
+};
+
+// Inner levels a 4-way tree over n triangles needs at least (leaves hold <= 4).
+uint32_t min_levels(size_t n) {
+  uint32_t l = 0;
+  while (n > 4) { n = (n + 3) / 4; ++l; }
+  return l;
+}
+
+struct WalkBuilder {
+  BuiltMesh& m;
+  std::vector<WItem> items;
+  std::vector<uint32_t> leaf_first;  // per reference leaf: its first sorted index
+  uint32_t n_tris = 0, max_depth = 10, depth = 0, next_rec = 0;
+
+  // Binned SAH cut of items[b, e) (n >= 2): returns the cut position in (b, e), items partitioned.
+  size_t split(size_t b, size_t e) {
+    constexpr int kBins = 32;
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = b; i < e; ++i)
+      for (int k = 0; k < 3; ++k) { cmin[k] = std::min(cmin[k], items[i].c[k]); cmax[k] = std::max(cmax[k], items[i].c[k]); }
+    double best = INFINITY;
+    int best_axis = -1, best_bin = 0;
+    for (int axis = 0; axis < 3; ++axis) {
+      const float ext = cmax[axis] - cmin[axis];
+      if (!(ext > 0.0f)) continue;
+      Box3 bb[kBins];
+      size_t cnt[kBins] = {};
+      const float scale = kBins / ext;
+      for (size_t i = b; i < e; ++i) {
+        int k = (int)((items[i].c[axis] - cmin[axis]) * scale);
+        k = std::min(std::max(k, 0), kBins - 1);
+        bb[k].grow(items[i]);
+        cnt[k]++;
+      }
+      Box3 right[kBins];
+      size_t rc[kBins] = {};
+      Box3 acc;
+      size_t an = 0;
+      for (int k = kBins - 1; k > 0; --k) {
+        acc.grow(bb[k]);
+        an += cnt[k];
+        right[k] = acc;
+        rc[k] = an;
+      }
+      Box3 left;
+      size_t ln = 0;
+      for (int k = 0; k < kBins - 1; ++k) {  // cut after bin k
+        left.grow(bb[k]);
+        ln += cnt[k];
+        if (ln == 0 || rc[k + 1] == 0) continue;
+        const double cost = left.area() * (double)ln + right[k + 1].area() * (double)rc[k + 1];
+        if (cost < best) { best = cost; best_axis = axis; best_bin = k; }
+      }
+    }
+    if (best_axis < 0) return b + (e - b) / 2;  // every centroid equal: any cut
+    const float scale = kBins / (cmax[best_axis] - cmin[best_axis]);
+    const int axis = best_axis, bin = best_bin;
+    auto mid = std::partition(items.begin() + (long)b, items.begin() + (long)e, [&](const WItem& t) {
+      int k = (int)((t.c[axis] - cmin[axis]) * scale);
+      k = std::min(std::max(k, 0), kBins - 1);
+      return k <= bin;
+    });
+    const size_t cut = (size_t)(mid - items.begin());
+    return (cut > b && cut < e) ? cut : b + (e - b) / 2;
+  }
+
+  // Four parts of items[b, e) by count (median splits along the widest centroid axis): the
+  // fallback that keeps the depth within max_depth.
+  void quarter(size_t b, size_t e, size_t cut[5]) {
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = b; i < e; ++i)
+      for (int k = 0; k < 3; ++k) { cmin[k] = std::min(cmin[k], items[i].c[k]); cmax[k] = std::max(cmax[k], items[i].c[k]); }
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (cmax[k] - cmin[k] > cmax[axis] - cmin[axis]) axis = k;
+    const size_t n = e - b;
+    for (int q = 0; q <= 4; ++q) cut[q] = b + n * (size_t)q / 4;
+    auto less = [axis](const WItem& x, const WItem& y) { return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.tri < y.tri); };
+    std::nth_element(items.begin() + (long)b, items.begin() + (long)cut[2], items.begin() + (long)e, less);
+    std::nth_element(items.begin() + (long)b, items.begin() + (long)cut[1], items.begin() + (long)cut[2], less);
+    std::nth_element(items.begin() + (long)cut[2], items.begin() + (long)cut[3], items.begin() + (long)e, less);
+  }
+
+  uint32_t leaf(size_t b, size_t e) {
+    const uint32_t first = n_tris + next_rec;  // record index in m.leaves (after the sorted ones)
+    for (size_t i = b; i < e; ++i, ++next_rec) {
+      const uint32_t t = items[i].tri;
+      const float* src = &m.leaves[kTriFloats * (size_t)t];
+      float* dst = &m.leaves[kTriFloats * (size_t)(n_tris + next_rec)];
+      std::memcpy(dst, src, kTriFloats * sizeof(float));  // v0 v1 v2, reference leaf, lane, sorted index
+    }
+    return (1u << 31) | ((uint32_t)(e - b) << 27) | first;
+  }
+
+  uint32_t build(size_t b, size_t e, uint32_t level, Box3& box_out) {
+    const size_t n = e - b;
+    box_out = Box3();
+    for (size_t i = b; i < e; ++i) box_out.grow(items[i]);
+    if (n <= 4) return leaf(b, e);
+    depth = std::max(depth, level + 1);
+    size_t cut[5];
+    if (level + 1 + min_levels((n + 3) / 4) >= max_depth) {  // no slack left: balanced quarters
+      quarter(b, e, cut);
+    } else {  // greedy: split the part with the largest area x count until there are four
+      struct Part { size_t b, e; double cost; };
+      std::vector<Part> parts{{b, e, 0.0}};
+      while (parts.size() < 4) {
+        int pick = -1;
+        double most = -1.0;
+        for (int k = 0; k < (int)parts.size(); ++k) {
+          if (parts[k].e - parts[k].b < 2) continue;
+          Box3 pb;
+          for (size_t i = parts[k].b; i < parts[k].e; ++i) pb.grow(items[i]);
+          const double c = pb.area() * (double)(parts[k].e - parts[k].b);
+          if (c > most) { most = c; pick = k; }
+        }
+        const size_t pb = parts[pick].b, pe = parts[pick].e, pc = split(pb, pe);
+        parts[pick] = {pb, pc, 0.0};
+        parts.insert(parts.begin() + pick + 1, Part{pc, pe, 0.0});
+      }
+      for (int q = 0; q < 4; ++q) cut[q] = parts[q].b;
+      cut[4] = e;
+    }
+    Box3 cb[4];
+    uint32_t ch[4];
+    for (int q = 0; q < 4; ++q) ch[q] = build(cut[q], cut[q + 1], level + 1, cb[q]);
+    DevNode node{};
+    for (int q = 0; q < 4; ++q) {  // exact f32 boxes; push ranks unused by the front-to-back walk
+      node.lo[q][0] = cb[q].lo[0]; node.lo[q][1] = cb[q].hi[0]; node.lo[q][2] = cb[q].lo[1]; node.lo[q][3] = cb[q].hi[1];
+      node.hi[q][0] = cb[q].lo[2]; node.hi[q][1] = cb[q].hi[2];
+      std::memcpy(&node.hi[q][2], &ch[q], 4);
+      const uint32_t zero = 0;
+      std::memcpy(&node.hi[q][3], &zero, 4);
+    }
+    m.nodes.push_back(node);
+    return (uint32_t)m.nodes.size() - 1;
+  }
+};
+
+}  // namespace
+
+void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
+  const auto t0 = std::chrono::steady_clock::now();
+  WalkBuilder w{m};
+  w.n_tris = (uint32_t)(m.leaves.size() / kTriFloats);
+  w.max_depth = max_depth;
+  w.items.resize(w.n_tris);
+  for (uint32_t t = 0; t < w.n_tris; ++t) {
+    const float* r = &m.leaves[kTriFloats * (size_t)t];
+    WItem& it = w.items[t];
+    for (int k = 0; k < 3; ++k) {
+      it.lo[k] = std::min(std::min(r[k], r[3 + k]), r[6 + k]);
+      it.hi[k] = std::max(std::max(r[k], r[3 + k]), r[6 + k]);
+      it.c[k] = 0.5f * (it.lo[k] + it.hi[k]);
+    }
+    it.tri = t;
+  }
+  m.leaves.resize(2 * m.leaves.size());
+  Box3 root_box;
+  const uint32_t root = w.build(0, w.n_tris, 0, root_box);
+  if (root >> 31) {  // a single leaf (<= 4 triangles): keep walking the reference tree
+    m.leaves.resize(m.leaves.size() / 2);
+    return;
+  }
+  m.walk_root = root;
+  m.walk_nodes = (uint32_t)m.nodes.size() - m.ref_nodes;
+  m.walk_depth = w.depth;
+  m.walk_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace yart_dev

@@ -69,7 +69,8 @@ class SceneInfo(C.Structure):
                 ("bvh_nodes", C.c_uint32), ("bvh_leaves", C.c_uint32), ("bvh_max_depth", C.c_uint32),
                 ("bvh_max_stack", C.c_uint32), ("device_bytes", C.c_uint64), ("world_nodes", C.c_uint32),
                 ("world_depth", C.c_uint32), ("bvh_tied_cuts", C.c_uint32), ("bvh_tied_leaves", C.c_uint32),
-                ("bvh_build_ms", C.c_double), ("upload_ms", C.c_double)]
+                ("bvh_build_ms", C.c_double), ("upload_ms", C.c_double), ("walk_nodes", C.c_uint32),
+                ("walk_depth", C.c_uint32)]
 
 
 class QbvhBuildInfo(C.Structure):
