@@ -1,7 +1,9 @@
-"""World-size-2 gloo run of the multi-GPU data path on CPU: each rank renders its pixel blocks
-(with the CPU restatement standing in for the device kernel, same (shard_index, shard_count)
-rule), and yart.shard.assemble_frame — the reduce bench.py issues over RCCL — assembles rank 0's
-frame, which must equal the single-process render bitwise."""
+"""World-size 2 and 3 gloo runs of the multi-GPU data path on CPU: each rank renders its pixel
+blocks (the CPU restatement standing in for the device kernel, same (shard_index, shard_count)
+rule) and the frame is assembled on rank 0 three ways — the packed-shard gather bench.py issues
+(libyart's ncclGather wire format, restated by yart.shard.PackedGather), and the two test-only
+reference forms (a full-frame reduce, a pixel-index gather). Each must equal the single-process
+render bitwise."""
 import os
 import socket
 

@@ -3,7 +3,7 @@
 #   tools/kres.sh [path/to/kernels.hip]
 HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=${1:-$HERE/../yet-another-raytracer_amd/csrc/kernels.hip}
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -I"$HERE/../build/gen" \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -I"$HERE/../build/gen" ${KDEFS:-} \
   --cuda-device-only -c -o /dev/null "$SRC" -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import re, sys
 cur = None; rows = {}

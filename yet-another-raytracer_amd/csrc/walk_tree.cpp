@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -46,12 +47,14 @@ uint32_t min_levels(size_t n) {
 struct WalkBuilder {
   BuiltMesh& m;
   std::vector<WItem> items;
-  std::vector<uint32_t> leaf_first;  // per reference leaf: its first sorted index
   uint32_t n_tris = 0, max_depth = 10, depth = 0, next_rec = 0;
+  int bins = 32;  // SAH bins per axis (YART_WALK_BINS, A/B)
+  int pick = 0;   // which part the greedy 4-way expansion splits next: 0 area x count, 1 count, 2 area (YART_WALK_PICK)
 
   // Binned SAH cut of items[b, e) (n >= 2): returns the cut position in (b, e), items partitioned.
   size_t split(size_t b, size_t e) {
-    constexpr int kBins = 32;
+    constexpr int kMaxBins = 128;
+    const int kBins = bins;
     float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t i = b; i < e; ++i)
       for (int k = 0; k < 3; ++k) { cmin[k] = std::min(cmin[k], items[i].c[k]); cmax[k] = std::max(cmax[k], items[i].c[k]); }
@@ -60,8 +63,8 @@ struct WalkBuilder {
     for (int axis = 0; axis < 3; ++axis) {
       const float ext = cmax[axis] - cmin[axis];
       if (!(ext > 0.0f)) continue;
-      Box3 bb[kBins];
-      size_t cnt[kBins] = {};
+      Box3 bb[kMaxBins];
+      size_t cnt[kMaxBins] = {};
       const float scale = kBins / ext;
       for (size_t i = b; i < e; ++i) {
         int k = (int)((items[i].c[axis] - cmin[axis]) * scale);
@@ -69,8 +72,8 @@ struct WalkBuilder {
         bb[k].grow(items[i]);
         cnt[k]++;
       }
-      Box3 right[kBins];
-      size_t rc[kBins] = {};
+      Box3 right[kMaxBins];
+      size_t rc[kMaxBins] = {};
       Box3 acc;
       size_t an = 0;
       for (int k = kBins - 1; k > 0; --k) {
@@ -142,18 +145,19 @@ struct WalkBuilder {
       struct Part { size_t b, e; double cost; };
       std::vector<Part> parts{{b, e, 0.0}};
       while (parts.size() < 4) {
-        int pick = -1;
+        int sel = -1;
         double most = -1.0;
         for (int k = 0; k < (int)parts.size(); ++k) {
           if (parts[k].e - parts[k].b < 2) continue;
           Box3 pb;
           for (size_t i = parts[k].b; i < parts[k].e; ++i) pb.grow(items[i]);
-          const double c = pb.area() * (double)(parts[k].e - parts[k].b);
-          if (c > most) { most = c; pick = k; }
+          const double cnt = (double)(parts[k].e - parts[k].b);
+          const double c = pick == 1 ? cnt : pick == 2 ? pb.area() : pb.area() * cnt;
+          if (c > most) { most = c; sel = k; }
         }
-        const size_t pb = parts[pick].b, pe = parts[pick].e, pc = split(pb, pe);
-        parts[pick] = {pb, pc, 0.0};
-        parts.insert(parts.begin() + pick + 1, Part{pc, pe, 0.0});
+        const size_t pb = parts[sel].b, pe = parts[sel].e, pc = split(pb, pe);
+        parts[sel] = {pb, pc, 0.0};
+        parts.insert(parts.begin() + sel + 1, Part{pc, pe, 0.0});
       }
       for (int q = 0; q < 4; ++q) cut[q] = parts[q].b;
       cut[4] = e;
@@ -181,6 +185,8 @@ void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
   WalkBuilder w{m};
   w.n_tris = (uint32_t)(m.leaves.size() / kTriFloats);
   w.max_depth = max_depth;
+  if (const char* e = std::getenv("YART_WALK_BINS")) w.bins = std::min(128, std::max(2, std::atoi(e)));
+  if (const char* e = std::getenv("YART_WALK_PICK")) w.pick = std::atoi(e);
   w.items.resize(w.n_tris);
   for (uint32_t t = 0; t < w.n_tris; ++t) {
     const float* r = &m.leaves[kTriFloats * (size_t)t];

@@ -1,14 +1,18 @@
-"""Pixel-block sharding across ranks and the one collective that assembles the frame.
+"""Pixel-block sharding across ranks and the collectives that assemble the frame (Python side).
 
 Block b (8x8 pixels, row-major over ceil(W/8) x ceil(H/8)) belongs to rank b % world — the rule
-libyart.so's k_render applies to (shard_index, shard_count) and the oracle restates. Every rank
-renders only its own blocks into a zeroed full-frame buffer. Two ways to assemble rank dst's frame:
+libyart.so's k_render applies to (shard_index, shard_count) and the oracle restates.
 
-* `assemble_frame`: ONE reduce(SUM) of the full frames — exact, since each pixel has exactly one
-  non-zero contributor; simple, but every rank ships W*H*24 bytes through the ring.
-* `ShardGather`: each rank packs its own pixels (1/world of the frame) and ONE gather to dst
-  collects them over the point-to-point xGMI links, where they are scattered back into place —
-  the same bits, world x less data (the xGMI links are per peer, so the gather is one hop each).
+On the product path the frame is assembled inside libyart (yart_gather_frame_async: ONE
+ncclGather of block-packed shards + k_unpack_shards; yart_render_multi_async for one process
+driving N devices). What lives here:
+
+* `PackedGather` — the same packets and unpack restated over torch.distributed, for backends
+  libyart cannot drive: bench.py's gloo rehearsal on one device and its torch-RCCL fallback;
+* `packed_pixels`, `block_owner`, `covered_axis` — the layout, for tests;
+* `assemble_frame` (a full-frame reduce) and `ShardGather` (pixel-index gather) — TEST-ONLY
+  reference forms the CPU tests (tests/test_distributed.py) check the packed gather against; no
+  product path uses them.
 """
 import numpy as np
 import torch
