@@ -29,7 +29,7 @@ CONFIGS = {
 }
 
 
-def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False):
+def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False, pmc=None):
     p = yart.Preset(scene_name)
     cam = p.camera(w, h)
     ts = time.perf_counter()
@@ -91,7 +91,17 @@ def run(name, scene_name, w, h, spp, depth, shard=(0, 1), stats=True, cpu=False)
         ff, bf = tf / F64_VALU_PEAK_TFLOPS, gbs / HBM_PEAK_GBS
         line["roofline"] = {"flop_tflops_modelled": round(tf, 3), "flop_frac": round(ff, 4),
                             "alg_bytes": int(nbytes), "alg_GBps": round(gbs, 1), "alg_bytes_frac_of_hbm": round(bf, 4),
+                            "alg_bytes_note": "SURVEY 8(d) record bytes; for meshes served from L2 / Infinity Cache, "
+                                              "not HBM (see hbm_counter)",
                             "bound": ("hbm (algorithmic bytes)" if bf > ff else "valu (f64)") if mesh else "valu (f64)"}
+        if pmc:  # HBM bytes the counters saw for a render of this same frame (rocprofv3, tools/gpu_round_end.sh)
+            pm = json.loads(Path(pmc).read_text())
+            hb = pm.get("hbm_bytes_per_launch")
+            if hb:
+                line["hbm_counter"] = {"bytes_per_launch": int(hb), "GBps": round(hb / (ms * 1e-3) / 1e9, 1),
+                                       "frac_of_hbm": round(hb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "over_alg_bytes": round(hb / nbytes, 3), "kernel": pm.get("kernel"),
+                                       "source": f"{pmc} (FETCH_SIZE x 2 + WRITE_SIZE per launch, MI355X_MICROARCH.md HBM)"}
     if cpu:
         import oracle_lib as O
         cspp = max(1, spp // 64)
@@ -109,13 +119,16 @@ def main():
     ap.add_argument("--spp-scale", type=float, default=1.0)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--pmc", action="append", default=[],
+                    help="CFG=path: rocprofv3 PMC summary (tools/summarize_profiles.py) of a render of that config's frame")
     a = ap.parse_args()
+    pmc = dict(x.split("=", 1) for x in a.pmc)
     for c in a.configs.split(","):
         scene, w, h, spp, depth = CONFIGS[c]
         spp = max(1, int(spp * a.spp_scale))
         if c == "C5":
             run(c + "-shard", scene, w, h, spp, depth, shard=(0, 8), stats=not a.no_stats, cpu=False)
-        run(c, scene, w, h, spp, depth, stats=not a.no_stats, cpu=a.cpu)
+        run(c, scene, w, h, spp, depth, stats=not a.no_stats, cpu=a.cpu, pmc=pmc.get(c))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round evidence at HEAD (one gpurun call; every GPU step under its own time limit, the script
+# stops at the first failure):
+#   pytest   the -m gpu suite
+#   smoke    __graft_entry__.smoke()
+#   bench    bench.py with the driver's arguments
+#   prof_cornell  rocprofv3 trace + FETCH / WRITE / VALU / mix passes over bench.py (cornell, C2)
+#   prof_c4 / prof_c5  trace + FETCH / WRITE passes over the C4 / C5 frames tools/bench_configs.py
+#            times at --spp-scale 0.0625 (bunny 800x800x32, david 1920x1080x64)
+#   configs  tools/bench_configs.py over every BASELINE config; with PMC summaries of the C4 / C5
+#            frames present in profiles/ (tools/summarize_profiles.py), the counter HBM bytes too
+# Raw outputs under gpurun_out/; tools/summarize_profiles.py turns them into profiles/ files.
+set -u
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$REPO/gpurun_out; mkdir -p "$OUT"; cd "$REPO"
+TAG=${TAG:-r03}
+run() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n ${TAILN:-4} "$OUT/$name.log"
+  [ $rc -eq 0 ] || { echo "stopping after rc=$rc"; exit $rc; }
+}
+STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_c4 prof_c5 configs"}
+for s in $STEPS; do
+  case $s in
+    pytest) run ${TAG}_gpu_tests 900 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
+    prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
+    prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
+    prof_c5) PFX=c5_ PROG="tools/render_once.py david 1920 1080 64 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
+    configs)
+      PM=""
+      [ -f profiles/${TAG}_c4_pmc.json ] && PM="$PM --pmc C4=profiles/${TAG}_c4_pmc.json"
+      [ -f profiles/${TAG}_c5_pmc.json ] && PM="$PM --pmc C5=profiles/${TAG}_c5_pmc.json"
+      run ${TAG}_bench_configs 900 python3 tools/bench_configs.py --spp-scale 0.0625 $PM ;;
+  esac
+done
+echo ALL_OK

@@ -2005,7 +2005,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   // SORT (YART_SORT, the plain list kernel): each iteration's camera rays and material scatters are
   // regrouped across the workgroup's 4 waves by task through LDS, so a wave runs one branch for
   // (nearly) all its lanes instead of every branch any of its lanes takes (kernels.hip, below).
-  constexpr bool SORT = YART_SORT && !HAS_MESH && !BVH && DYN && !EXT && !LPF;
+  constexpr bool SORT = YART_SORT == 1 && !HAS_MESH && !BVH && DYN && !EXT && !LPF;
   __shared__ double s_sd[SORT ? 11 * 256 : 1];
   __shared__ uint32_t s_su[SORT ? 6 * 256 : 1];
   __shared__ uint32_t s_cnt[SORT ? 16 : 1];
@@ -2117,7 +2117,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
     }
     const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
-    if constexpr (SORT) {  // the workgroup leaves together: the regrouping below synchronizes it
+    if constexpr (SORT || (YART_SORT == 2 && !HAS_MESH && !BVH && DYN && !EXT)) {  // the workgroup leaves together
       if (!__syncthreads_or(run)) break;
     } else {
       if (__ballot(run) == 0) break;
@@ -2158,6 +2158,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         T = *Tp / pdf_val;
       }
     };
+#if YART_SORT == 2
+    // diagnostic (A/B only): the regrouping's barriers alone, the work done in place
+    if constexpr (!HAS_MESH && !BVH && DYN && !EXT) {
+      __syncthreads();
+      __syncthreads();
+    }
+#endif
     if constexpr (SORT) {
       // Task per lane: 0 camera ray, 1 Lambertian, 2 Metal, 3 Dielectric scatter, 4 none. Slots
       // in task order (then wave, then lane) across the workgroup; lane k of the workgroup runs
