@@ -20,13 +20,14 @@ run() {
   echo "== $name rc=$rc"; tail -n ${TAILN:-4} "$OUT/$name.log"
   [ $rc -eq 0 ] || { echo "stopping after rc=$rc"; exit $rc; }
 }
-STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_c4 prof_c5 configs"}
+STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_david prof_c4 prof_c5 configs"}
 for s in $STEPS; do
   case $s in
     pytest) run ${TAG}_gpu_tests 900 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
+    prof_david) PFX=david_ PROG="tools/render_once.py david 960 540 16 2" PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
     prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
     prof_c5) PFX=c5_ PROG="tools/render_once.py david 1920 1080 64 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
     configs)

@@ -1978,9 +1978,6 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
 #ifndef YART_REGEN_MIN
 #define YART_REGEN_MIN 1
 #endif
-#ifndef YART_SORT
-#define YART_SORT 0
-#endif
 #ifndef YART_LPF
 #define YART_LPF 0
 #endif
@@ -2002,13 +1999,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH, JOBL3 = YART_JOBL && DYN && HAS_MESH;
   __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : JOBL3 ? 4 * 3 * 64 : 1];
   __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
-  // SORT (YART_SORT, the plain list kernel): each iteration's camera rays and material scatters are
-  // regrouped across the workgroup's 4 waves by task through LDS, so a wave runs one branch for
-  // (nearly) all its lanes instead of every branch any of its lanes takes (kernels.hip, below).
-  constexpr bool SORT = YART_SORT == 1 && !HAS_MESH && !BVH && DYN && !EXT && !LPF;
-  __shared__ double s_sd[SORT ? 11 * 256 : 1];
-  __shared__ uint32_t s_su[SORT ? 6 * 256 : 1];
-  __shared__ uint32_t s_cnt[SORT ? 16 : 1];
   // the wave index through readfirstlane: uniform, so the per-wave LDS bases live in SGPRs (as a
   // VGPR the mesh walk's stack base was spilled and reloaded at every pop)
   const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2117,11 +2107,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       }
     }
     const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
-    if constexpr (SORT || (YART_SORT == 2 && !HAS_MESH && !BVH && DYN && !EXT)) {  // the workgroup leaves together
-      if (!__syncthreads_or(run)) break;
-    } else {
-      if (__ballot(run) == 0) break;
-    }
+    if (__ballot(run) == 0) break;
     double R = 0.0;
     bool term = false, want = false;
     // LPF: a Lambertian scatter's mixture pdf waits for the world pass of the ray it sampled,
@@ -2158,126 +2144,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         T = *Tp / pdf_val;
       }
     };
-#if YART_SORT == 2
-    // diagnostic (A/B only): the regrouping's barriers alone, the work done in place
-    if constexpr (!HAS_MESH && !BVH && DYN && !EXT) {
-      __syncthreads();
-      __syncthreads();
-    }
-#endif
-    if constexpr (SORT) {
-      // Task per lane: 0 camera ray, 1 Lambertian, 2 Metal, 3 Dielectric scatter, 4 none. Slots
-      // in task order (then wave, then lane) across the workgroup; lane k of the workgroup runs
-      // slot k: the camera lanes and each material's lanes sit together in (mostly) whole waves.
-      uint32_t task = 4u;
-      if (run) {
-        if (fresh) task = 0u;
-        else {
-          const uint32_t kind = S.materials[hmat].kind;
-          task = kind == YART_MAT_LAMBERTIAN ? 1u : kind == YART_MAT_METAL ? 2u : 3u;
-        }
-      }
-      uint32_t rank = 0;
-#pragma unroll
-      for (uint32_t t = 0; t < 4; ++t) {
-        const uint64_t mt = __ballot(task == t);
-        if (lane == 0) s_cnt[wave * 4 + t] = (uint32_t)__popcll(mt);
-        if (task == t) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mt, 0u));
-      }
-      __syncthreads();
-      uint32_t tot[4], all = 0;
-#pragma unroll
-      for (uint32_t t = 0; t < 4; ++t) tot[t] = s_cnt[t] + s_cnt[4 + t] + s_cnt[8 + t] + s_cnt[12 + t];
-      uint32_t slot_of = 0;
-      if (task < 4u) {
-        uint32_t base = 0;
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) base += t < task ? tot[t] : 0u;
-        for (uint32_t w = 0; w < wave; ++w) base += s_cnt[w * 4 + task];
-        slot_of = base + rank;
-        const uint32_t k = slot_of;
-        s_su[k] = jl[0]; s_su[256 + k] = jl[64]; s_su[512 + k] = depth; s_su[768 + k] = hmat;
-        s_su[1024 + k] = jl[256]; s_su[1280 + k] = jl[320];
-        s_sd[k] = T; s_sd[256 + k] = ray.d.x; s_sd[512 + k] = ray.d.y; s_sd[768 + k] = ray.d.z; s_sd[1024 + k] = ray.wl;
-        s_sd[1280 + k] = hp.x; s_sd[1536 + k] = hp.y; s_sd[1792 + k] = hp.z;
-        s_sd[2048 + k] = hn.x; s_sd[2304 + k] = hn.y; s_sd[2560 + k] = hn.z;
-      }
-#pragma unroll
-      for (uint32_t t = 0; t < 4; ++t) all += tot[t];
-      __syncthreads();
-      const uint32_t k = threadIdx.x;  // this lane's slot in the regrouped order
-      if (k < all) {
-        const uint32_t kt = k < tot[0] ? 0u : k < tot[0] + tot[1] ? 1u : k < tot[0] + tot[1] + tot[2] ? 2u : 3u;
-        const uint32_t kpix = s_su[k], ksmp = s_su[256 + k], kdepth = s_su[512 + k];
-        Rng gs;
-        gs.k0 = (uint32_t)A.seed; gs.k1 = (uint32_t)(A.seed >> 32);
-        rng_phase<true>(gs, kpix, ksmp, kt == 0u ? 0u : A.max_depth - kdepth + 1u);
-        double oT, oR = 0.0;
-        V3 oo, od;
-        uint32_t odepth;
-        bool oterm = false;
-        double owl = s_sd[1024 + k];
-        if (kt == 0u) {  // main.rs:692-698
-          OCC(OCC_FRESH);
-          const uint32_t jx = s_su[1024 + k], jy = s_su[1280 + k];
-          const double tx = (double)jx + gen_f64(gs);
-          const double u = tx / (double)(W - 1);
-          const double ty = (double)jy + gen_f64(gs);
-          const double v = 1.0 - ty / (double)(H - 1);
-          const double wl = gen_range(gs, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
-          const Ray r = camera_ray(*kernarg_camera(), u, v, wl, gs, false);
-          oT = 1.0; oo = r.o; od = r.d; odepth = A.max_depth; owl = wl;
-        } else {  // scatter at the stored hit (material.rs), main.rs:548-584
-          Ray kr;
-          kr.o = mk(0.0, 0.0, 0.0);
-          kr.d = mk(s_sd[256 + k], s_sd[512 + k], s_sd[768 + k]);
-          kr.wl = owl; kr.time = 0.0;
-          const double kT = s_sd[k];
-          const V3 khp = mk(s_sd[1280 + k], s_sd[1536 + k], s_sd[1792 + k]);
-          const V3 khn = mk(s_sd[2048 + k], s_sd[2304 + k], s_sd[2560 + k]);
-          const uint32_t kmat = s_su[768 + k];
-          const int kbin = spectrum_bin(owl);
-          double nTp = 0.0, ncosv = 0.0;
-          bool npend;
-          typename MathPolicy<HAS_MESH, BVH, EXT>::type fm;
-          scatter_at<EXT, STATS, LPF>(S, fm, gs, khp, khn, kmat, 0.0, 0.0, kbin, kr, kT, kdepth, st, oT, oo, od, odepth, oR,
-                                      oterm, nTp, ncosv, npend);
-          if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
-            rng_phase<true>(gs, kpix, ksmp, A.max_depth - kdepth + 1u);
-            Ieee im;
-            scatter_at<EXT, STATS, LPF>(S, im, gs, khp, khn, kmat, 0.0, 0.0, kbin, kr, kT, kdepth, st, oT, oo, od, odepth,
-                                        oR, oterm, nTp, ncosv, npend);
-          }
-        }
-        s_sd[k] = oT; s_sd[256 + k] = oo.x; s_sd[512 + k] = oo.y; s_sd[768 + k] = oo.z;
-        s_sd[1024 + k] = od.x; s_sd[1280 + k] = od.y; s_sd[1536 + k] = od.z; s_sd[1792 + k] = owl; s_sd[2048 + k] = oR;
-        s_su[k] = odepth; s_su[256 + k] = oterm ? 1u : 0u;
-      }
-      __syncthreads();
-      if (task < 4u) {
-        const uint32_t k2 = slot_of;
-        T = s_sd[k2]; ray.o = mk(s_sd[256 + k2], s_sd[512 + k2], s_sd[768 + k2]);
-        ray.d = mk(s_sd[1024 + k2], s_sd[1280 + k2], s_sd[1536 + k2]);
-        R = s_sd[2048 + k2];
-        depth = s_su[k2];
-        term = s_su[256 + k2] != 0u;
-        if (task == 0u) {
-          ray.wl = s_sd[1792 + k2];
-          ray.time = 0.0;
-          wbin = spectrum_bin(ray.wl);
-          fresh = false;
-        }
-        if (!term) {
-          if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
-            R = T * 1.0;
-            term = true;
-          } else {
-            want = true;
-          }
-        }
-      }
-      __syncthreads();  // the slots are rewritten next iteration
-    } else if (run) {
+    if (run) {
       OCC(OCC_ITER);
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
