@@ -376,13 +376,19 @@ int yart_intersect(yart_scene* scene, const double* rays, uint32_t n, double* hi
  * arrays (FNV-1a 64 over node records, triangle records, leaf records, normals), so builder
  * variants can be compared byte for byte. flags: YART_QBVH_TIES_DESC orders equal centroid
  * keys by descending input index instead of ascending (the probe of sort_unstable_by's freedom,
- * qbvh.rs:679-685); YART_QBVH_SERIAL builds on one thread. */
+ * qbvh.rs:679-685); YART_QBVH_SERIAL builds on one thread; YART_QBVH_WALK also builds the
+ * front-to-back walk's SAH tree (as scene creation does) and checks its structure: every triangle
+ * in exactly one walk leaf, every box holding what is below it, four non-empty children per inner
+ * node, the depth within the 32-slot stack (walk_valid = 1). */
 #define YART_QBVH_TIES_DESC 1u
 #define YART_QBVH_SERIAL 2u
+#define YART_QBVH_WALK 4u
 typedef struct yart_qbvh_build_info {
   uint32_t nodes, leaves, depth, tied_cuts, tied_leaves, reserved;
   uint64_t digest;
   double build_ms;
+  uint32_t walk_nodes, walk_depth, walk_valid, walk_reserved;
+  double walk_build_ms;
 } yart_qbvh_build_info;
 int yart_qbvh_build(const float* positions, const double* normals, uint32_t n_triangles, uint32_t flags,
                     yart_qbvh_build_info* out);

@@ -50,3 +50,18 @@ def test_degenerate_meshes_are_refused(meshes):
         yart.qbvh_build(pos[:4], nrm[:4])
     yart.qbvh_build(pos, nrm)  # a successful call clears yart_last_error (thread-local)
     assert yart.load_device().yart_last_error().decode() == ""
+
+
+@pytest.mark.parametrize("name", ["cube", "david", "sycee"])
+def test_walk_tree_structure(meshes, name):
+    """The front-to-back walk's SAH tree (walk_tree.cpp, built at scene creation): every triangle
+    in exactly one walk leaf with its record (vertices, reference leaf, lane, sorted index) intact,
+    every child box inside its parent's and non-empty, four children per inner node, the depth
+    within the 32-slot stack (3 depth + 1 <= 32); deterministic (threaded == sequential build)."""
+    pos, nrm = meshes[name]
+    w = yart.qbvh_build(pos, nrm, yart.QBVH_WALK)
+    assert w["walk_valid"] == 1
+    assert w["walk_nodes"] > 0 and 3 * w["walk_depth"] + 1 <= 32
+    assert w["nodes"] == MESHES[name][1]  # the reference tree's shape is unchanged
+    assert yart.qbvh_build(pos, nrm, yart.QBVH_WALK | yart.QBVH_SERIAL)["digest"] == w["digest"]
+    assert yart.qbvh_build(pos, nrm)["digest"] != w["digest"]

@@ -48,5 +48,9 @@ bool build_qbvh(uint32_t n_tris, const float* positions, const double* normals, 
 // (kernels.hip, qbvh_coop). Every inner node has four non-empty children; depth <= max_depth (the
 // traversal stack holds 3 depth + 1 entries).
 void build_walk_tree(BuiltMesh& m, uint32_t max_depth);
+// Structural check of the walk tree (yart_qbvh_build YART_QBVH_WALK; tests): every triangle in
+// exactly one walk leaf with its record intact, every box inside its parent's, four non-empty
+// children per inner node, depth <= max_depth.
+bool check_walk_tree(const BuiltMesh& m, uint32_t max_depth);
 
 }  // namespace yart_dev

@@ -405,6 +405,12 @@ int yart_qbvh_build(const float* positions, const double* normals, uint32_t n, u
   opt.ties_desc = (flags & YART_QBVH_TIES_DESC) != 0;
   opt.threads = (flags & YART_QBVH_SERIAL) ? 1u : 0u;
   if (!build_qbvh(n, positions, normals, b, err, opt)) return fail(YART_ERR_UNSUPPORTED, err);
+  uint32_t walk_max = 0;
+  if (flags & YART_QBVH_WALK) {  // as scene creation builds it, then its structural check
+    const uint32_t slots = 3 * b.depth + 1 > (uint32_t)kStackSlots ? (uint32_t)kMaxStackSlots : (uint32_t)kStackSlots;
+    walk_max = (slots - 1) / 3;
+    build_walk_tree(b, walk_max);
+  }
   uint64_t h = 1469598103934665603ull;  // FNV-1a 64
   auto mix = [&h](const void* p, size_t len) {
     const unsigned char* c = (const unsigned char*)p;
@@ -415,13 +421,17 @@ int yart_qbvh_build(const float* positions, const double* normals, uint32_t n, u
   mix(b.aux.data(), b.aux.size() * sizeof(LeafAux));
   mix(b.normals.data(), b.normals.size() * sizeof(double));
   std::memset(out, 0, sizeof *out);
-  out->nodes = (uint32_t)b.nodes.size();
+  out->nodes = b.ref_nodes;
   out->leaves = (uint32_t)b.aux.size();
   out->depth = b.depth;
   out->tied_cuts = b.tied_cuts;
   out->tied_leaves = b.tied_leaves;
   out->digest = h;
   out->build_ms = b.build_ms;
+  out->walk_nodes = b.walk_nodes;
+  out->walk_depth = b.walk_depth;
+  out->walk_valid = (flags & YART_QBVH_WALK) && check_walk_tree(b, walk_max) ? 1u : 0u;
+  out->walk_build_ms = b.walk_build_ms;
   return ok();
 }
 

@@ -211,4 +211,48 @@ void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
   m.walk_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+bool check_walk_tree(const BuiltMesh& m, uint32_t max_depth) {
+  if (m.walk_nodes == 0) return false;
+  const uint32_t n = (uint32_t)(m.leaves.size() / kTriFloats / 2);
+  std::vector<uint8_t> seen(n, 0);
+  bool ok = true;
+  uint32_t deepest = 0;
+  struct Item { uint32_t id, level; float lo[3], hi[3]; };
+  std::vector<Item> st{{m.walk_root, 0, {-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}}};
+  while (!st.empty() && ok) {
+    const Item it = st.back();
+    st.pop_back();
+    if (it.id >> 31) {  // a leaf: its records lie inside the box its parent stores for it
+      const uint32_t count = (it.id >> 27) & 0xFu, first = it.id & ((1u << 27) - 1u);
+      ok = count >= 1 && count <= 4 && first >= n && first + count <= 2 * n;
+      for (uint32_t i = 0; ok && i < count; ++i) {
+        const float* r = &m.leaves[kTriFloats * (size_t)(first + i)];
+        uint32_t tri;
+        std::memcpy(&tri, &r[11], 4);
+        ok = tri < n && !seen[tri] && std::memcmp(r, &m.leaves[kTriFloats * (size_t)tri], kTriFloats * sizeof(float)) == 0;
+        if (ok) seen[tri] = 1;
+        for (int v = 0; ok && v < 3; ++v)
+          for (int k = 0; k < 3; ++k) ok = r[3 * v + k] >= it.lo[k] && r[3 * v + k] <= it.hi[k];
+      }
+      continue;
+    }
+    ok = it.id >= m.ref_nodes && it.id < m.nodes.size();
+    if (!ok) break;
+    deepest = std::max(deepest, it.level + 1);
+    const DevNode& nd = m.nodes[it.id];
+    for (int q = 0; q < 4 && ok; ++q) {
+      Item c;
+      std::memcpy(&c.id, &nd.hi[q][2], 4);
+      c.level = it.level + 1;
+      c.lo[0] = nd.lo[q][0]; c.hi[0] = nd.lo[q][1]; c.lo[1] = nd.lo[q][2]; c.hi[1] = nd.lo[q][3];
+      c.lo[2] = nd.hi[q][0]; c.hi[2] = nd.hi[q][1];
+      for (int k = 0; k < 3; ++k)  // non-empty, and inside its parent's box
+        ok = ok && c.lo[k] <= c.hi[k] && c.lo[k] >= it.lo[k] && c.hi[k] <= it.hi[k];
+      st.push_back(c);
+    }
+  }
+  for (uint32_t t = 0; ok && t < n; ++t) ok = seen[t] != 0;
+  return ok && deepest == m.walk_depth && deepest <= max_depth;
+}
+
 }  // namespace yart_dev

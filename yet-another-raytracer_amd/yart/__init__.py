@@ -239,7 +239,7 @@ class DeviceScene:
         return hits, obj
 
 
-QBVH_TIES_DESC, QBVH_SERIAL = 1, 2
+QBVH_TIES_DESC, QBVH_SERIAL, QBVH_WALK = 1, 2, 4
 
 
 def load_obj(path, with_uv=False):
@@ -261,7 +261,7 @@ def qbvh_build(positions, normals, flags=0):
     normals = np.ascontiguousarray(normals, np.float64)
     info = abi.QbvhBuildInfo()
     _check_dev(load_device().yart_qbvh_build(_ptr(positions), _ptr(normals), len(positions), flags, C.byref(info)))
-    return {k: getattr(info, k) for k, _ in info._fields_ if k != "reserved"}
+    return {k: getattr(info, k) for k, _ in info._fields_ if "reserved" not in k}
 
 
 def finalize_rgba8(xyz_sum, spp, device=0):

@@ -76,7 +76,8 @@ class SceneInfo(C.Structure):
 class QbvhBuildInfo(C.Structure):
     _fields_ = [("nodes", C.c_uint32), ("leaves", C.c_uint32), ("depth", C.c_uint32), ("tied_cuts", C.c_uint32),
                 ("tied_leaves", C.c_uint32), ("reserved", C.c_uint32), ("digest", C.c_uint64),
-                ("build_ms", C.c_double)]
+                ("build_ms", C.c_double), ("walk_nodes", C.c_uint32), ("walk_depth", C.c_uint32),
+                ("walk_valid", C.c_uint32), ("walk_reserved", C.c_uint32), ("walk_build_ms", C.c_double)]
 
 
 class RenderStats(C.Structure):
