@@ -1339,6 +1339,21 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // meshes are walked cooperatively (qbvh_coop) by the whole wave, the other objects per lane.
 // LPF: objects holding a light-pdf slot are tested with the capture forms (rect_t_cap /
 // sphere_t_cap: the same t and answer as prim_t, plus the [t_min, inf) test pdf_value makes).
+// A wave-uniform read of a scene table (the list walk's object, a light of the mixture pdf): the
+// index made uniform by readfirstlane and the table read through the constant address space, so
+// the record arrives by scalar loads into SGPRs. Read as a plain global, the loads after the
+// loop's scratch stores were vector loads (the compiler cannot prove them unclobbered) and every
+// field of the record took a VGPR.
+template <class T>
+__device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
+#ifdef YART_VECTOR_SCENE
+  return base[i];
+#else
+  typedef const __attribute__((address_space(4))) T* cptr;
+  return *(const T*)((cptr)base + __builtin_amdgcn_readfirstlane(i));
+#endif
+}
+
 template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
@@ -1347,7 +1362,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
   for (uint32_t i = 0; i < S.n_objects; ++i) {
-    const DevObject& o = S.objects[i];
+    const DevObject& o = uniform_at(S.objects, i);
     const uint32_t kind = o.kind, nxf = o.n_xf;
     const bool medium = EXT && nxf != 0 && o.xf_kind[0] == YART_XF_MEDIUM;
     if (HAS_MESH && kind == YART_PRIM_MESH && !medium) {  // wave-uniform
@@ -1355,7 +1370,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-      qbvh_coop<STATS, SLOTS>(S.meshes[o.mesh], want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
+      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1848,6 +1863,43 @@ __device__ unsigned long long g_occ[32];
 #else
 #define OCC(k) do {} while (0)
 #endif
+// Cycle probe (debug builds with -DYART_PROF only, tools/cycles.py): the shader clock (s_memtime)
+// around each region; whichever lanes run it, the first active lane adds the region's cycles to its
+// wave's LDS counter (a divergent region is timed once per wave execution), and the waves' counters
+// are added into g_prof at exit. Regions nest (the material branches sit inside PF_SCATTER).
+enum { PF_LOOP, PF_ASSIGN, PF_RNG, PF_CAMERA, PF_SCATTER, PF_LAMB, PF_METAL, PF_DIEL, PF_WORLD, PF_SHADE, PF_TERM,
+       PF_WAVES, PF_N };
+#ifdef YART_PROF
+__device__ unsigned long long g_prof[16];
+__shared__ unsigned long long s_prof[4 * PF_N];
+struct ProfScope {
+  int k;
+  uint64_t t0;
+  __device__ explicit ProfScope(int k_) : k(k_), t0(__builtin_amdgcn_s_memtime()) {}
+  __device__ ~ProfScope() {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))
+      atomicAdd(&s_prof[(threadIdx.x >> 6) * PF_N + k], (unsigned long long)(t1 - t0));
+  }
+};
+#define PROF_CAT2(a, b) a##b
+#define PROF_CAT(a, b) PROF_CAT2(a, b)
+#define PROF(k) const ProfScope PROF_CAT(prof_, __LINE__)(k)
+#else
+#define PROF(k) do {} while (0)
+#endif
+// Marginal-cost probe (debug builds with -DYART_DUP=k only, tools/dup_cost.py): region k (1 camera,
+// 2 scatter, 3 world pass, 4 sample end, 5 the iteration's Philox blocks) runs g_dup times per
+// execution, its inputs and outputs laundered so the repeats are neither merged nor dead; the frame
+// time's slope in g_dup is what one execution of the region costs the kernel.
+#ifdef YART_DUP
+__device__ uint32_t g_dup = 1;
+#define DUP_LOOP(k) for (uint32_t dup_i = 0, dup_n = (YART_DUP == (k) ? __builtin_amdgcn_readfirstlane(g_dup) : 1u); dup_i < dup_n; ++dup_i)
+#define DUP_LAUNDER(x) asm volatile("" : "+v"(x))
+#else
+#define DUP_LOOP(k)
+#define DUP_LAUNDER(x) do {} while (0)
+#endif
 
 // Material::scatter at the stored hit + the mixture pdf (material.rs, main.rs:548-584): the path's
 // next ray and throughput, or its end. One body for both math policies (the Fast cores first; a
@@ -1866,6 +1918,7 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
     const uint32_t kind = m.kind;
     if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
       OCC(OCC_LAMB);
+      PROF(PF_LAMB);
       // the albedo is looked up where it is multiplied in: fetched here, it was held (and
       // spilled) through the direction sampling and the light pdfs
       auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
@@ -1893,7 +1946,7 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
         } else {
           const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
           double sum = -0.0;
-          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(S.lights[i], hp, dir, ray.wl, st, mp);
+          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ray.wl, st, mp);
           pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
         }
       }
@@ -1929,6 +1982,7 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       depth_ = depth - 1;
     } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
       OCC(OCC_METAL);
+      PROF(PF_METAL);
       const V3 reflected = reflect(mp.unit(ray.d), hn);
       V3 p;
       for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
@@ -1943,6 +1997,7 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       depth_ = depth - 1;
     } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
       OCC(OCC_DIEL);
+      PROF(PF_DIEL);
       const double wl2 = ray.wl * ray.wl;
       const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
       const double n = mp.sqrt(n2);
@@ -2048,11 +2103,16 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   double hu = 0.0, hv = 0.0;            // its texture coordinates (EXT)
   int wbin = 0;                         // spectrum bin of the path's wavelength
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
+#ifdef YART_PROF
+  if (lane < PF_N) s_prof[wave * PF_N + lane] = 0ull;
+#endif
 
   // The loop exits wave-uniformly: a lane without work stays in it with `run` false, so the
   // mesh walk (qbvh_coop) is reached by all 64 lanes together.
   for (;;) {
+    PROF(PF_LOOP);
     if (DYN) {
+      PROF(PF_ASSIGN);
       uint64_t m = drained ? 0ull : __ballot(need);
 #if YART_REGEN_MIN > 1
       // Regeneration threshold (A/B flag): lanes whose path ended wait, idle, until at least
@@ -2122,7 +2182,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       const double weight = 1.0 / (double)S.n_lights;
       double sum = -0.0;
       for (uint32_t i = 0; i < S.n_lights; ++i) {
-        const DevObject& L = S.lights[i];
+        const DevObject& L = uniform_at(S.lights, i);
         double v = 0.0;
         if (L.lpf < kMaxLpf) {  // wave-uniform
           if (STATS) st.v[ST_LIGHT]++;
@@ -2149,9 +2209,26 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
-      rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
+      {
+        PROF(PF_RNG);
+        DUP_LOOP(5) {
+        DUP_LAUNDER(g.k0);
+        rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
+        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3);
+        DUP_LAUNDER(g.b4); DUP_LAUNDER(g.b5); DUP_LAUNDER(g.b6); DUP_LAUNDER(g.b7);
+        }
+      }
       if (fresh) {  // main.rs:692-698
         OCC(OCC_FRESH);
+        PROF(PF_CAMERA);
+#ifdef YART_DUP
+        const Rng g_dup0 = g;
+#endif
+        DUP_LOOP(1) {
+#ifdef YART_DUP
+        g = g_dup0;
+        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3);
+#endif
         uint32_t jx = x, jy = y;
         if (JOBL) { jx = jl[256]; jy = jl[320]; }
         if (JOBL3) { const uint32_t p = jl[0]; jy = p / W; jx = p - jy * W; }
@@ -2167,10 +2244,14 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
         wbin = spectrum_bin(wl);
 #endif
+        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.o.y); DUP_LAUNDER(ray.o.z);
+        DUP_LAUNDER(ray.d.x); DUP_LAUNDER(ray.d.y); DUP_LAUNDER(ray.d.z); DUP_LAUNDER(ray.wl); DUP_LAUNDER(wbin);
+        }
         T = 1.0;
         depth = A.max_depth;
         fresh = false;
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
+        PROF(PF_SCATTER);
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
         auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
@@ -2183,7 +2264,19 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         uint32_t ndepth;
         bool nterm, npend;
         typename MathPolicy<HAS_MESH, BVH, EXT>::type fm;
+#ifdef YART_DUP
+        const Rng g_dup0 = g;
+        DUP_LOOP(2) {
+        g = g_dup0;
+        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3); DUP_LAUNDER(T);
+        fm = typename MathPolicy<HAS_MESH, BVH, EXT>::type{};
         scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
+        DUP_LAUNDER(nT); DUP_LAUNDER(no.x); DUP_LAUNDER(no.y); DUP_LAUNDER(no.z); DUP_LAUNDER(nd.x); DUP_LAUNDER(nd.y);
+        DUP_LAUNDER(nd.z); DUP_LAUNDER(nR); DUP_LAUNDER(ndepth);
+        }
+#else
+        scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
+#endif
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
           rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, A.max_depth - depth + 1u);
           Ieee im;
@@ -2211,10 +2304,20 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       bool scat = false;
       const QueryCtx q{g.k0, g.k1, JL ? jl[64] : smp, JL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
+        PROF(PF_WORLD);
+        DUP_LOOP(3) {
+        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+        DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
+        }
       } else if (want) {
         OCC(OCC_WALK);
+        PROF(PF_WORLD);
+        DUP_LOOP(3) {
+        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
         hit = world_hit<HAS_MESH, BVH, STATS, EXT, LPF>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q, &cap);
+        DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
+        }
       }
       if (LPF && want && pend) {
         resolve(cap);
@@ -2224,6 +2327,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         }
       }
       if (want && !term) {
+        PROF(PF_SHADE);
         if (STATS) st.v[ST_SEGMENTS]++;
         if (!hit) {
           R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
@@ -2252,6 +2356,9 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     }
     if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
       OCC(OCC_TERM);
+      PROF(PF_TERM);
+      DUP_LOOP(4) {
+      DUP_LAUNDER(R); DUP_LAUNDER(ray.wl);
       double cx, cy, cz;
       cie_xyz(ray.wl, cx, cy, cz);
       double sx = cx * R, sy = cy * R, sz = cz * R;
@@ -2270,6 +2377,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           jsl = (py & 7u) * 8u + (px & 7u);
         }
         double* q = A.scratch + 3 * (((size_t)jb * A.s_count + (js - A.s_begin)) * 64 + jsl);
+        DUP_LAUNDER(sx); DUP_LAUNDER(sy); DUP_LAUNDER(sz);
         q[0] = sx; q[1] = sy; q[2] = sz;
         need = true;
       } else {
@@ -2277,6 +2385,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         smp++;
         if (smp < s_stop) fresh = true;
         else alive = false;
+      }
       }
     }
   }
@@ -2292,6 +2401,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     for (int i = 0; i < kNumStats; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
   }
+#ifdef YART_PROF
+  if (lane < PF_WAVES) atomicAdd(&g_prof[lane], s_prof[wave * PF_N + lane]);
+  if (lane == 0) atomicAdd(&g_prof[PF_WAVES], 1ull);
+#endif
 }
 
 // ------------------------------------------------------------- wavefront path (mesh scenes)
@@ -2753,6 +2866,22 @@ extern "C" int yart_debug_occupancy(int device, unsigned long long* out32) {
   if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(yart_dev::g_occ), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
   unsigned long long z[32] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_occ), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef YART_PROF
+extern "C" int yart_debug_cycles(int device, unsigned long long* out16) {  // reads and clears g_prof
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(yart_dev::g_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef YART_DUP
+extern "C" int yart_debug_set_dup(int device, unsigned int n) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_dup), &n, sizeof n) == hipSuccess ? 0 : -1;
 }
 #endif
 
