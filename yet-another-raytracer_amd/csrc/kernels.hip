@@ -1933,8 +1933,17 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
         if (gen_range(g, 0.0, 1.0) < 0.5) {
           // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
           OCC(OCC_LAMB_LIGHT);
+#ifndef YART_LIGHT_K_LANE
+          if (S.n_lights <= 2) {  // k = 0 for every lane (gen_index(g, 1) draws nothing): scalar loads
+            dir = light_random(uniform_at(S.lights, 0u), hp, g, mp);
+          } else {
+            const uint32_t k = (uint32_t)gen_index(g, S.n_lights - 1);
+            dir = light_random(S.lights[k], hp, g, mp);
+          }
+#else
           const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
           dir = light_random(S.lights[k], hp, g, mp);
+#endif
         } else {
           OCC(OCC_LAMB_COS);
           dir = local(uvw, random_cosine_direction(g, mp));
