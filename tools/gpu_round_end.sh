@@ -5,6 +5,7 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py with the driver's arguments
 #   prof_cornell  rocprofv3 trace + FETCH / WRITE / VALU / mix passes over bench.py (cornell, C2)
+#   prof_cornell_more  stall / memory-instruction passes over bench.py (not in the default steps)
 #   prof_c4 / prof_c5  trace + FETCH / WRITE passes over the C4 / C5 frames tools/bench_configs.py
 #            times at --spp-scale 0.0625 (bunny 800x800x32, david 1920x1080x64)
 #   configs  tools/bench_configs.py over every BASELINE config; with PMC summaries of the C4 / C5
@@ -27,6 +28,7 @@ for s in $STEPS; do
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
+    prof_cornell_more) PFX=cornell_ PASSES="stall mem" bash tools/profile.sh || exit 1 ;;
     prof_david) PFX=david_ PROG="tools/render_once.py david 960 540 16 2" PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
     prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
     prof_c5) PFX=c5_ PROG="tools/render_once.py david 1920 1080 64 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
