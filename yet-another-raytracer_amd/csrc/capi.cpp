@@ -342,6 +342,7 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   if (use_world) {
     HIP_TRY(upload(s->owned, world.nodes.data(), world.nodes.size(), &ds.world_nodes, bytes), "upload world nodes");
     HIP_TRY(upload(s->owned, world.objs.data(), world.objs.size(), &ds.world_objs, bytes), "upload world objects");
+    HIP_TRY(upload(s->owned, world.sph.data(), world.sph.size(), &ds.world_sph, bytes), "upload world spheres");
     ds.n_world_nodes = (uint32_t)world.nodes.size();
   }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;

@@ -111,8 +111,9 @@ struct alignas(16) DevWorldNode {
   float bmax[3];
   uint32_t count;   // 0 = inner node
   uint32_t first;   // inner: left child (right = first + 1); leaf: first slot in world_objs
-  uint32_t pad[3];
+  uint32_t pad[3];  // pad[0]: leaf flags (kWorldLeafSpheres)
 };
+constexpr uint32_t kWorldLeafSpheres = 1u;  // every object of the leaf is a sphere without wrappers
 static_assert(sizeof(DevWorldNode) == 48, "DevWorldNode must be 48 B");
 
 struct DevScene {
@@ -124,6 +125,7 @@ struct DevScene {
   const double* background;  // 36 bins
   const DevWorldNode* world_nodes;  // null: walk the list linearly
   const uint32_t* world_objs;
+  const double* world_sph;   // per world_objs slot: centre xyz, radius (plain spheres; else 0)
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
   uint32_t has_mesh;
   uint32_t has_ext;  // noise/image textures, isotropic materials, media or moving spheres (EXT kernels)

@@ -1468,6 +1468,9 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
 // (~1e-7 relative) stays far inside m — over [t_min, closest] widened by 2^-10, so it never
 // drops a node holding a hit the scan would accept (ties included). Non-finite rays take the
 // list walk.
+#ifndef YART_WORLD_SPH
+#define YART_WORLD_SPH 1
+#endif
 template <bool STATS>
 __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
                                                   uint32_t* stk, Stats& st) {
@@ -1494,7 +1497,21 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
     const DevWorldNode& N = S.world_nodes[node];
     const uint32_t count = N.count, first = N.first;
     bool pop = true;
-    if (count) {
+    if (count && YART_WORLD_SPH && (N.pad[0] & kWorldLeafSpheres)) {
+      // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
+      // object records and the kind switch; the same sphere_t on the same values
+      for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t i = S.world_objs[first + k];
+        const double* sp = S.world_sph + 4 * (size_t)(first + k);
+        if (STATS) st.v[ST_PRIM]++;
+        double t;
+        if (sphere_t(sp, r, tmin, closest, t) && (!found || t < closest || i > id.obj)) {
+          closest = t;
+          id.obj = i; id.sub = 0; id.u = 0.0; id.v = 0.0;
+          found = true;
+        }
+      }
+    } else if (count) {
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t i = S.world_objs[first + k];
         const DevObject& ob = S.objects[i];

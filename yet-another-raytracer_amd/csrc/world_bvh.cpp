@@ -205,6 +205,23 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
   build(items, 0, items.size(), 0, 0, out, sah, prm);
   // the device walk pushes at most one entry per level into its kStackSlots-deep stack
   if (sah && out.depth >= (uint32_t)kStackSlots) return build_world_bvh(objs, out, false);
+  // Leaves whose objects are all plain spheres (no wrapper) get kWorldLeafSpheres: the walk reads
+  // their centre and radius from the compact per-slot records instead of the object records.
+  out.sph.assign(4 * out.objs.size(), 0.0);
+  for (size_t j = 0; j < out.objs.size(); ++j) {
+    const DevObject& o = objs[out.objs[j]];
+    if (o.kind == YART_PRIM_SPHERE && o.n_xf == 0)
+      for (int k = 0; k < 4; ++k) out.sph[4 * j + k] = o.p[k];
+  }
+  for (DevWorldNode& n : out.nodes) {
+    if (n.count == 0) continue;
+    bool all = true;
+    for (uint32_t k = 0; k < n.count; ++k) {
+      const DevObject& o = objs[out.objs[n.first + k]];
+      all = all && o.kind == YART_PRIM_SPHERE && o.n_xf == 0;
+    }
+    n.pad[0] = all ? kWorldLeafSpheres : 0u;
+  }
   return out.depth < (uint32_t)kStackSlots;
 }
 

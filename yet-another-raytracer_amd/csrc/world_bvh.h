@@ -11,6 +11,7 @@ namespace yart_dev {
 struct BuiltWorld {
   std::vector<DevWorldNode> nodes;  // root = nodes[0]
   std::vector<uint32_t> objs;       // leaf slots -> object index
+  std::vector<double> sph;          // per leaf slot: centre xyz, radius of a plain sphere (else 0)
   uint32_t depth = 0;               // inner levels on the deepest root-to-leaf path
 };
 
