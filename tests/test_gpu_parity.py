@@ -283,6 +283,42 @@ def test_world_bvh_ties_go_to_the_later_object(dev):
         _hits_equal(h, o, h2, o2)
 
 
+def test_world_bvh_sphere_leaves_beside_wrapped_and_hollow_spheres(dev):
+    """Leaves of plain spheres take the compact-record walk (kWorldLeafSpheres); spheres under a
+    Translate, hollow (negative-radius) spheres and a rect share the list, so some leaves mix the
+    two paths. Closest hits and a render stay bitwise the linear scan's."""
+    b = O.DescBuilder()
+    mats = [b.material(abi.MAT_LAMBERTIAN, b.texture((0.2 * k, 0.4, 0.6))) for k in range(3)]
+    glass = b.material(abi.MAT_DIELECTRIC, b=(1.04, 0.23, 1.01), c=(0.006, 0.02, 103.56))
+    rng = np.random.default_rng(23)
+    for k in range(60):
+        c = tuple(rng.uniform(-6, 6, 3))
+        r = float(rng.uniform(0.2, 0.9))
+        if k % 5 == 1:
+            b.obj(abi.PRIM_SPHERE, mats[k % 3], (0.0, 0.0, 0.0, r), xforms=[(abi.XF_TRANSLATE, c)])
+        elif k % 7 == 2:
+            b.obj(abi.PRIM_SPHERE, glass, c + (-r,))  # hollow: the radius is negative
+        else:
+            b.obj(abi.PRIM_SPHERE, mats[k % 3], c + (r,))
+    b.obj(abi.PRIM_XZ_RECT, mats[1], (-7.0, 7.0, -7.0, 7.0, -6.5))
+    b.obj(abi.PRIM_SPHERE, mats[0], (0.0, 2.0, 0.0, 1.5), light=True)
+    b.obj(abi.PRIM_SPHERE, b.material(abi.MAT_DIFFUSE_LIGHT, b.texture((8.0, 8.0, 8.0))), (0.0, 9.0, 0.0, 1.5))
+    d = b.desc()
+    rays = _random_rays(60000, -8, 8, seed=29)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    with pytest.MonkeyPatch.context() as mp:
+        mp.setenv("YART_WORLD_BVH", "1")
+        s = yart.DeviceScene(d)
+        assert s.info().world_nodes > 0
+        h, o = s.intersect(rays)
+        assert (o2 >= 0).mean() > 0.15
+        _hits_equal(h, o, h2, o2)
+        W, H, spp = 40, 32, 4
+        cam = yart.make_camera((0.0, 3.0, 16.0), (0.0, 0.0, 0.0), 40.0, W / H, 0.0, 10.0)
+        np.testing.assert_array_equal(s.render(cam, yart.render_params(W, H, spp, 50)),
+                                      O.OracleScene(d).render(cam, yart.render_params(W, H, spp, 50)))
+
+
 def test_moving_spheres_match_oracle(dev):
     """MovingSphere + the shutter-time draw it switches on (camera.rs:91), with a glass one."""
     from test_scene_features import moving_scene
