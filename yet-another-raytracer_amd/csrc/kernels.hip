@@ -887,14 +887,19 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
 //    ~2^44: a ray within ~1e-13 rad of the triangle's plane). Rays with a zero, NaN or infinite
 //    direction or origin component, where the monotonicity argument does not hold, walk in the
 //    reference order from the start.
-struct CoopRay { double o[3], d[3], inv[3], tmax; };  // result: o = (t, u, v), d[0] = found << 32 | tri
+// The ray's f32 box-test constants are formed once, when the wave stages its rays (every lane its
+// own, in parallel), not in take() by the whole wave each time a quad starts a ray. The f64 1/d
+// they come from is formed again where it is needed: the exact final check and the reference
+// order. flags: bit 0 front to back allowed, bits 1-3 the ray octant.
+struct CoopRay { double o[3], d[3], tmax; float c32[6], inv32[3]; uint32_t flags; };
+typedef uint16_t CoopEnt;  // a stack entry's box entry, the upper half of the f32, rounded down
 constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
-// Per-quad stack slots (node id + its f32 box entry): 32 for meshes of depth <= 10 (3 depth + 1
+// Per-quad stack slots (node id + its box entry, CoopEnt): 32 for meshes of depth <= 10 (3 depth + 1
 // entries at most), 64 — the reference's own stack (qbvh.rs:382-384) — for deeper ones, which only
 // the wavefront trace kernel walks (k_wf_trace<64>, 3 waves per SIMD for the larger LDS).
 constexpr int kCoopSlots = kStackSlots;
 constexpr int kDeepSlots = kMaxStackSlots;
-template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS * 16 * 8; }
+template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS * 16 * (4 + (int)sizeof(CoopEnt)); }
 template <int SLOTS> constexpr int wave_lds_words() {
   return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
 }
@@ -993,29 +998,51 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
-  float* qent = reinterpret_cast<float*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
+  CoopEnt* qent = reinterpret_cast<CoopEnt*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
   const uint32_t n = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  if (want) {
-    CoopRay& s = rays[rank];
-    s.o[0] = r.o.x; s.o[1] = r.o.y; s.o[2] = r.o.z;
-    s.d[0] = r.d.x; s.d[1] = r.d.y; s.d[2] = r.d.z;
-    s.inv[0] = 1.0 / r.d.x; s.inv[1] = 1.0 / r.d.y; s.inv[2] = 1.0 / r.d.z;
-    s.tmax = tmax_in;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
   const __attribute__((address_space(1))) LeafAux* aux = (const __attribute__((address_space(1))) LeafAux*)M.aux;
   const uint32_t root = M.root, wroot = M.wroot;  // reference tree / walk tree (front to back)
   const float extent = M.extent;
+  if (want) {
+    CoopRay& s = rays[rank];
+    s.o[0] = r.o.x; s.o[1] = r.o.y; s.o[2] = r.o.z;
+    s.d[0] = r.d.x; s.d[1] = r.d.y; s.d[2] = r.d.z;
+    s.tmax = tmax_in;
+    const double so[3] = {r.o.x, r.o.y, r.o.z}, sdir[3] = {r.d.x, r.d.y, r.d.z};
+    double iv[3];
+    bool ok = aux != nullptr && extent < 1e15f;
+    double O = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      iv[j] = 1.0 / sdir[j];
+      // front to back needs finite, non-zero direction components (the slab entries of nested
+      // boxes are then monotone) and magnitudes the f32 test holds without overflow
+      ok = ok && sdir[j] != 0.0 && fabs(so[j]) < 1e15 && fabs(iv[j]) < 1e15;
+      O = fmax(O, fabs(so[j]));
+    }
+    const double m = ((double)extent + O) * 0x1p-20;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double a = -(so[j] * iv[j]), dl = iv[j] > 0.0 ? m * iv[j] : -(m * iv[j]);
+      const double sdl = iv[j] > 0.0 ? dl : -dl;
+      s.inv32[j] = (float)iv[j];
+      s.c32[2 * j] = (float)(a - sdl);
+      s.c32[2 * j + 1] = (float)(a + sdl);
+    }
+    s.flags = (ok ? 1u : 0u) | (ray_octant(sdir) << 1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
-  double ro[3], rd[3], inv[3], tin = 0.0, tb = 0.0, teff = 0.0;
-  float inv32[3], tmin32 = 0.0f, teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
+  double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
+  const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
+  float inv32[3], teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
   uint32_t pos = 0, node = 0, bleaf = 0, bkey = 0;
@@ -1034,28 +1061,16 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   };
   auto take = [&]() {
     const CoopRay& s = rays[ray];
-    bool ok = aux != nullptr && extent < 1e15f;
-    double O = 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      ro[j] = s.o[j]; rd[j] = s.d[j]; inv[j] = s.inv[j];
-      // front to back needs finite, non-zero direction components (the slab entries of nested
-      // boxes are then monotone) and magnitudes the f32 test holds without overflow
-      ok = ok && rd[j] != 0.0 && fabs(ro[j]) < 1e15 && fabs(inv[j]) < 1e15;
-      O = fmax(O, fabs(ro[j]));
+      ro[j] = s.o[j]; rd[j] = s.d[j];
+      inv32[j] = s.inv32[j];
+      c32[j] = vfloat2{s.c32[2 * j], s.c32[2 * j + 1]};
     }
-    const double m = ((double)extent + O) * 0x1p-20;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double a = -(ro[j] * inv[j]), dl = inv[j] > 0.0 ? m * inv[j] : -(m * inv[j]);
-      const double sd = inv[j] > 0.0 ? dl : -dl;
-      inv32[j] = (float)inv[j];
-      c32[j] = vfloat2{(float)(a - sd), (float)(a + sd)};
-    }
-    tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
+    const uint32_t fl = s.flags;
     tin = s.tmax;
-    pos = ray_octant(rd);
-    restart(ok);
+    pos = fl >> 1;
+    restart((fl & 1u) != 0u);
   };
   if (ray < n) take();
   if (STATS && lane == 0) st.v[ST_WALKS]++;
@@ -1148,6 +1163,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           ent = fminf(ent, 3.0e38f);
         } else {
           double l;
+          const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};  // the reference order (rare)
           hk = child_hit_l(lo, hi, ro, inv, tmin, teff, l);
           ent = 0.0f;  // unused in the reference order
         }
@@ -1175,7 +1191,10 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
 #endif
             {
               qstk[slot] = child;
-              qent[slot] = ent;
+              {  // rounded down: a dropped entry's true entry is beyond the bound too
+                const uint32_t eb = __float_as_uint(ent);
+                qent[slot] = (CoopEnt)((eb >> 16) + ((eb >> 31) & ((eb & 0xFFFFu) != 0u)));
+              }
             }
           }
           cursor += (int)__popc(ordered) - 1;
@@ -1191,7 +1210,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           if (cursor == 0) { fin = true; break; }
           cursor -= 1;
           node = qstk[cursor * 16 + (int)q];
-          if (!f2b || !(qent[cursor * 16 + (int)q] > bound)) break;
+          if (!f2b || !(__uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound)) break;
         }
       }
       if (fin && f2b && fnd) {
@@ -1201,7 +1220,8 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
         double l = tmin, h = tin;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const double t0 = ((double)A.lo[j] - ro[j]) * inv[j], t1 = ((double)A.hi[j] - ro[j]) * inv[j];
+          const double iv = 1.0 / rd[j];  // as formed at staging: the reference's slab test
+          const double t0 = ((double)A.lo[j] - ro[j]) * iv, t1 = ((double)A.hi[j] - ro[j]) * iv;
           l = fmax(l, fmin(t0, t1));
           h = fmin(h, fmax(t0, t1));
         }
