@@ -401,6 +401,10 @@ int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, u
  * 5 ln(a), 6 acos(a), 7 atan2(a,b) (3, 5-7: the deterministic fdlibm forms the kernels use). */
 int yart_probe_math(int device, int op, const double* a, const double* b, uint32_t n,
                     double* out);
+/* on != 0: every mesh ray whose front-to-back walk found a hit is walked again in the reference's
+ * order (the per-lane walk the exact post-walk check falls back to), for the frames rendered on
+ * this device until it is called with on = 0. The result is the same; only slower. */
+int yart_debug_force_rewalk(int device, int on);
 
 #ifdef __cplusplus
 }

@@ -203,6 +203,33 @@ def test_qbvh_tie_order_does_not_change_hits(dev, scene, render, monkeypatch):
     np.testing.assert_array_equal(ra, rb)
 
 
+@pytest.mark.parametrize("scene,render", [("david", ("david", 48, 27, 2)), ("sycee", ("bunny", 40, 40, 4))])
+def test_forced_rewalk_is_the_reference_answer(dev, scene, render):
+    """After the cooperative front-to-back walk, each lane checks its own ray's winner against the
+    reference's f64 box test; a ray that fails walks again in the reference's order, per lane
+    (qbvh_t). That path is almost never taken on real frames, so yart_debug_force_rewalk sends
+    every walk that found a hit down it: closest hits and renders stay bitwise the oracle's."""
+    p = yart.Preset(scene)
+    bounds = {"david": (-150, 250), "sycee": (-4, 4)}[scene]
+    rays = _random_rays(100000, *bounds, seed=41)
+    rp = yart.Preset(render[0])
+    cam, prm = rp.camera(render[1], render[2]), yart.render_params(render[1], render[2], render[3], 50)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    ref = O.OracleScene(rp.desc).render(cam, prm)
+    assert dev.yart_debug_force_rewalk(0, 1) == 0
+    try:
+        h, o = yart.DeviceScene(p.desc).intersect(rays)
+        rs = yart.DeviceScene(rp.desc)
+        img = rs.render(cam, prm)
+        _, st = rs.render_with_stats(cam, prm)
+    finally:
+        assert dev.yart_debug_force_rewalk(0, 0) == 0
+    assert (o2 >= 0).mean() > 0.05
+    _hits_equal(h, o, h2, o2)
+    np.testing.assert_array_equal(img, ref)
+    assert st.mesh_rewalks > 0
+
+
 def test_box_cull_is_exact_on_grazing_rays(dev):
     """The device's f32 box pre-test may only skip boxes no face of which is hit: rays aimed at
     box edges and corners, nudged by a few ulps to tiny offsets, must hit exactly as the oracle."""

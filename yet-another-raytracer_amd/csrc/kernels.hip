@@ -971,6 +971,12 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
   return (uint32_t)((k1 < key) | ((k1 == key) & ((c ^ 1u) < c))) + (uint32_t)((k2 < key) | ((k2 == key) & ((c ^ 2u) < c))) +
          (uint32_t)((k3 < key) | ((k3 == key) & ((c ^ 3u) < c)));
 }
+#ifndef YART_COOP_POSTCHECK
+#define YART_COOP_POSTCHECK 1
+#endif
+// Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
+// reference's order, so the rare path is exercised on whole frames.
+__device__ uint32_t g_force_rewalk;
 #ifndef YART_COOP_LEAF_MIN
 #define YART_COOP_LEAF_MIN 1  // quads waiting at a leaf before a round runs the leaf branch
 #endif
@@ -1038,6 +1044,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
+  // YART_COOP_POSTCHECK: W's exact check after the walk, per lane (the 32-slot walks only: the
+  // per-lane re-walk, qbvh_t, has a 32-slot stack)
+  constexpr bool kPostCheck = YART_COOP_POSTCHECK && SLOTS == kCoopSlots;
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
   double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
@@ -1213,7 +1222,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           if (!f2b || !(__uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound)) break;
         }
       }
-      if (fin && f2b && fnd) {
+      if (kPostCheck && fin && c == 0)  // the ray's own lane checks W after the walk (below)
+        rays[ray].flags = (f2b && fnd) ? (0x80000000u | bleaf) : 0u;
+      if (!kPostCheck && fin && f2b && fnd) {
         // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
         // (the f32 test visits a superset) and W's t is not before that box's entry (above)
         const auto& A = aux[bleaf];
@@ -1243,12 +1254,39 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  bool redo = false;
   if (want) {
     const CoopRay& s = rays[rank];
     const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
     found = (res >> 32) != 0;
     t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
     tri = (uint32_t)res;
+    const uint32_t fl = s.flags;
+    if (kPostCheck && (fl >> 31)) {
+      // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
+      // (the f32 test visits a superset) and W's t is not before that box's entry (above): each
+      // lane checks its own ray once, after the walk, instead of the whole wave at every ray's end.
+      const auto& A = aux[fl & 0x7FFFFFFFu];
+      const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+      double l = tmin, h = tmax_in;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double iv = 1.0 / rd[j];
+        const double t0 = ((double)A.lo[j] - ro[j]) * iv, t1 = ((double)A.hi[j] - ro[j]) * iv;
+        l = fmax(l, fmin(t0, t1));
+        h = fmin(h, fmax(t0, t1));
+      }
+      redo = !(h > l && t_hit >= l) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+    }
+  }
+  if (kPostCheck && __ballot(redo) != 0ull) {
+    // Rare: that ray walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in
+    // this wave's LDS, free now that every lane has read its record).
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (redo) {
+      if (STATS) st.v[ST_REWALK]++;
+      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
+    }
   }
 }
 
@@ -2930,6 +2968,12 @@ extern "C" int yart_debug_set_dup(int device, unsigned int n) {
   return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_dup), &n, sizeof n) == hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" int yart_debug_force_rewalk(int device, int on) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  const uint32_t v = on ? 1u : 0u;
+  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_force_rewalk), &v, sizeof v) == hipSuccess ? 0 : -1;
+}
 
 #ifdef YART_WALK_CHECK
 extern "C" int yart_debug_walk_fault(int device, unsigned int* out) {  // reads and clears the fault bits

@@ -92,6 +92,7 @@ def load_device():
     _sig(L, "yart_intersect", I, P, P, U32, P, P)
     _sig(L, "yart_probe_rng", I, I, U64, U32, U32, U32, P)
     _sig(L, "yart_probe_math", I, I, I, P, P, U32, P)
+    _sig(L, "yart_debug_force_rewalk", I, I, I)
     _sig(L, "yart_shard_packed_len", U64, U32, U32, U32, U32)
     _sig(L, "yart_render_packed_async", I, P, C.POINTER(abi.Camera), C.POINTER(abi.RenderParams), P, P)
     _sig(L, "yart_comm_unique_id", I, P)
