@@ -1,6 +1,7 @@
 // capi.cpp — the C ABI of include/yart.h: scene upload to HBM, launches, host conveniences.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -337,6 +338,20 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     dm[m].wroot = b.walk_root;
     dm[m].n_recs = (uint32_t)(b.leaves.size() / kTriFloats);
     dm[m].n_leaves = (uint32_t)b.aux.size();
+    {  // the cull box: union of the non-empty child boxes of the reference root and the walk root
+      float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (uint32_t r : {b.ref_nodes - 1, b.walk_root}) {
+        const DevNode& nd = b.nodes[r];
+        for (int k = 0; k < 4; ++k) {
+          const float mn[3] = {nd.lo[k][0], nd.lo[k][2], nd.hi[k][0]}, mx[3] = {nd.lo[k][1], nd.lo[k][3], nd.hi[k][1]};
+          if (!(std::isfinite(mn[0]) && std::isfinite(mn[1]) && std::isfinite(mn[2]))) continue;  // empty (+inf)
+          for (int j = 0; j < 3; ++j) { lo[j] = std::min(lo[j], mn[j]); hi[j] = std::max(hi[j], mx[j]); }
+        }
+      }
+      const float bl[4] = {lo[0], hi[0], lo[1], hi[1]}, bh[4] = {lo[2], hi[2], 0.0f, 0.0f};
+      std::memcpy(dm[m].box_lo, bl, sizeof bl);
+      std::memcpy(dm[m].box_hi, bh, sizeof bh);
+    }
   }
   HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
   if (use_world) {

@@ -99,6 +99,10 @@ struct DevMesh {
   uint32_t wroot;             // the walk tree's root (front to back; = root without a walk tree)
   uint32_t n_recs;            // triangle records (sorted + walk order)
   uint32_t n_leaves;          // reference leaves (LeafAux records)
+  // The union of both roots' child boxes, laid out as a DevNode child (lo = min x, max x, min y,
+  // max y; hi = min z, max z): a ray whose conservative f32 test misses it cannot pass any child
+  // box of either root, so it is left out of the cooperative walk (qbvh_coop).
+  float box_lo[4], box_hi[4];
 };
 
 // World BVH over the object list (not in the reference, whose HittableList is a linear scan):

@@ -900,12 +900,17 @@ constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
 constexpr int kCoopSlots = kStackSlots;
 constexpr int kDeepSlots = kMaxStackSlots;
 template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS * 16 * (4 + (int)sizeof(CoopEnt)); }
+#ifndef YART_COOP_PAIR
+#define YART_COOP_PAIR 0  // two consecutive instances of one mesh in one walk pool: measured slower
+#endif
+constexpr int kCoopOrderBytes = YART_COOP_PAIR ? 128 : 0;  // a paired walk's hand-out order, after the stacks
 template <int SLOTS> constexpr int wave_lds_words() {
-  return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
+  return ((coop_bytes<SLOTS>() + kCoopOrderBytes) / 4 > kStackSlots * 64) ? (coop_bytes<SLOTS>() + kCoopOrderBytes) / 4
+                                                                          : kStackSlots * 64;
 }
 constexpr int kCoopBytes = coop_bytes<kCoopSlots>();
 // LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
-constexpr int kWaveLdsWords = (kCoopBytes / 4 > kStackSlots * 64) ? kCoopBytes / 4 : kStackSlots * 64;
+constexpr int kWaveLdsWords = wave_lds_words<kCoopSlots>();
 constexpr double kF2bMargin = 0x1p-8;
 
 template <int CTRL>
@@ -974,6 +979,9 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 #ifndef YART_COOP_POSTCHECK
 #define YART_COOP_POSTCHECK 1
 #endif
+#ifndef YART_COOP_CULL
+#define YART_COOP_CULL 1  // rays missing the mesh's cull box stay out of the walk (qbvh_coop)
+#endif
 // Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
 // reference's order, so the rare path is exercised on whole frames.
 __device__ uint32_t g_force_rewalk;
@@ -994,63 +1002,179 @@ enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // pe
 __device__ unsigned int g_walk_fault;
 __device__ __forceinline__ void walk_fault(unsigned int bit) { atomicOr(&g_walk_fault, bit); }
 #endif
-template <bool STATS, int SLOTS = kCoopSlots>
+// A ray's walk record (CoopRay) formed by its own lane: the f32 box-test constants, the flags, and
+// whether the ray is walked at all (YART_COOP_CULL). A ray whose conservative test misses the
+// mesh's cull box (the union of both roots' child boxes) is left out of the walk: every child box
+// of either root lies inside that box, the f32 test passes on a box whenever it passes on a box
+// inside it (the fma bounds are monotone in the corners) and whenever the reference's f64 test
+// passes on it (child_hit_f32), so such a ray has no hit in the reference's walk either, and it
+// costs the pool no round.
+struct CoopStage { float inv32[3], c32[6]; uint32_t flags; bool walk; };
+__device__ __forceinline__ CoopStage coop_stage(const DevMesh& M, bool has_aux, const Ray& r, float tmin32, double tmax) {
+  CoopStage s;
+  const double so[3] = {r.o.x, r.o.y, r.o.z}, sdir[3] = {r.d.x, r.d.y, r.d.z};
+  const float extent = M.extent;
+  double iv[3];
+  bool ok = has_aux && extent < 1e15f;
+  double O = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    iv[j] = 1.0 / sdir[j];
+    // front to back needs finite, non-zero direction components (the slab entries of nested
+    // boxes are then monotone) and magnitudes the f32 test holds without overflow
+    ok = ok && sdir[j] != 0.0 && fabs(so[j]) < 1e15 && fabs(iv[j]) < 1e15;
+    O = fmax(O, fabs(so[j]));
+  }
+  const double m = ((double)extent + O) * 0x1p-20;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double a = -(so[j] * iv[j]), dl = iv[j] > 0.0 ? m * iv[j] : -(m * iv[j]);
+    const double sdl = iv[j] > 0.0 ? dl : -dl;
+    s.inv32[j] = (float)iv[j];
+    s.c32[2 * j] = (float)(a - sdl);
+    s.c32[2 * j + 1] = (float)(a + sdl);
+  }
+  s.flags = (ok ? 1u : 0u) | (ray_octant(sdir) << 1);
+  s.walk = true;
+#if YART_COOP_CULL
+  if (ok) {
+    const vfloat2 cc[3] = {vfloat2{s.c32[0], s.c32[1]}, vfloat2{s.c32[2], s.c32[3]}, vfloat2{s.c32[4], s.c32[5]}};
+    const float4 blo = make_float4(M.box_lo[0], M.box_lo[1], M.box_lo[2], M.box_lo[3]);
+    const float4 bhi = make_float4(M.box_hi[0], M.box_hi[1], 0.0f, 0.0f);
+    float ent;
+    s.walk = child_hit_f32(blo, bhi, s.inv32, cc, tmin32, (float)(tmax + fabs(tmax) * 0x1p-20), ent);
+  }
+#endif
+  return s;
+}
+__device__ __forceinline__ void coop_write(CoopRay& s, const Ray& r, double tmax, const CoopStage& g) {
+  s.o[0] = r.o.x; s.o[1] = r.o.y; s.o[2] = r.o.z;
+  s.d[0] = r.d.x; s.d[1] = r.d.y; s.d[2] = r.d.z;
+  s.tmax = tmax;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    s.inv32[j] = g.inv32[j];
+    s.c32[2 * j] = g.c32[2 * j];
+    s.c32[2 * j + 1] = g.c32[2 * j + 1];
+  }
+  s.flags = g.flags;
+}
+// The exact check of a front-to-back answer (below): W's reference leaf box passes the reference's
+// f64 test at t_max and W's t is not before that box's entry.
+__device__ __forceinline__ bool coop_check(const __attribute__((address_space(1))) LeafAux* aux, uint32_t leaf, const Ray& r,
+                                           double tmin, double tmax, double t) {
+  const auto& A = aux[leaf];
+  const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+  double l = tmin, h = tmax;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double iv = 1.0 / rd[j];
+    const double t0 = ((double)A.lo[j] - ro[j]) * iv, t1 = ((double)A.hi[j] - ro[j]) * iv;
+    l = fmax(l, fmin(t0, t1));
+    h = fmin(h, fmax(t0, t1));
+  }
+  return h > l && t >= l;
+}
+// PAIR: a lane whose first walk has finished saves that answer (the triangle, whether it hit, and
+// its exact check, made now) and forms its second record in place with t_max = the first answer.
+// Out of line: the pool reaches it a few times per walk, and inlined its temporaries crowded the
+// walk loop's registers.
+template <class R1>
+__device__ __noinline__ bool coop_restage(CoopRay& s, const DevMesh& M, const __attribute__((address_space(1))) LeafAux* aux,
+                                          const Ray& r, double tmin, float tmin32, double tmax_in, bool force, bool& f0,
+                                          uint32_t& tri0, bool& redo0, R1 r1);
+struct NoSecond { __device__ Ray operator()() const { return Ray{}; } };
+constexpr uint32_t kCoopDone = 0x40000000u;  // PAIR: a record's flags once its walk has finished
+template <class R1>
+__device__ __noinline__ bool coop_restage(CoopRay& s, const DevMesh& M, const __attribute__((address_space(1))) LeafAux* aux,
+                                          const Ray& r, double tmin, float tmin32, double tmax_in, bool force, bool& f0,
+                                          uint32_t& tri0, bool& redo0, R1 r1) {
+  const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
+  f0 = (res >> 32) != 0;
+  const double t0 = s.o[0];
+  tri0 = (uint32_t)res;
+  const uint32_t fl = s.flags;  // kCoopDone | the post-check request
+  redo0 = (fl >> 31) && (!coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t0) || force);
+  if (redo0) return false;  // walked again after the pool, and the second instance with it
+  const double c0 = f0 ? t0 : tmax_in;
+  const Ray rr = r1();
+  const CoopStage g1 = coop_stage(M, aux != nullptr, rr, tmin32, c0);
+  // the record keeps the first answer (o, d[0]) unless the second walk takes it over
+  if (g1.walk) coop_write(s, rr, c0, g1);
+  return g1.walk;
+}
+
+// PAIR (two consecutive list entries holding the same mesh, e.g. david's two statues,
+// scenes.rs:581-596): both walks share one pool. Entries of the second instance join it as the
+// first instance's walks finish — a finished ray's lane forms its second record (r1(): the ray in
+// the second instance's frame) with t_max = the first instance's answer, exactly the t_max the
+// list walk (hittable.rs:67-79) passes on — so the pool does not drain twice. Records are then
+// indexed by lane, and the pool's order is a byte list per wave after the stacks. The answer is
+// the list walk's: the second instance's hit if it has one (it is strictly nearer by its t_max),
+// else the first's; `inst` says which.
+template <bool STATS, int SLOTS = kCoopSlots, bool PAIR = false, class R1 = NoSecond>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
-                                       uint8_t* __restrict__ lds, Stats& st) {
+                                       uint8_t* __restrict__ lds, Stats& st, uint32_t* inst = nullptr, bool pair = false, R1 r1 = R1()) {
   found = false;
-  const uint64_t act = __ballot(want);
-  if (act == 0) return;
+  if (PAIR) *inst = 0u;
+  if (__ballot(want) == 0) return;
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
   CoopEnt* qent = reinterpret_cast<CoopEnt*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
-  const uint32_t n = (uint32_t)__popcll(act);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  uint8_t* order = lds + coop_bytes<SLOTS>();  // PAIR: the pool's records in hand-out order
   // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
   const __attribute__((address_space(1))) LeafAux* aux = (const __attribute__((address_space(1))) LeafAux*)M.aux;
   const uint32_t root = M.root, wroot = M.wroot;  // reference tree / walk tree (front to back)
-  const float extent = M.extent;
+  const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
+  // Each lane forms its own ray's record before the pool is laid out (coop_stage).
+  bool walk = false, walk1 = false;  // PAIR: walk1 = the second instance's record is in the pool
+  CoopStage g0{};
   if (want) {
-    CoopRay& s = rays[rank];
-    s.o[0] = r.o.x; s.o[1] = r.o.y; s.o[2] = r.o.z;
-    s.d[0] = r.d.x; s.d[1] = r.d.y; s.d[2] = r.d.z;
-    s.tmax = tmax_in;
-    const double so[3] = {r.o.x, r.o.y, r.o.z}, sdir[3] = {r.d.x, r.d.y, r.d.z};
-    double iv[3];
-    bool ok = aux != nullptr && extent < 1e15f;
-    double O = 0.0;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      iv[j] = 1.0 / sdir[j];
-      // front to back needs finite, non-zero direction components (the slab entries of nested
-      // boxes are then monotone) and magnitudes the f32 test holds without overflow
-      ok = ok && sdir[j] != 0.0 && fabs(so[j]) < 1e15 && fabs(iv[j]) < 1e15;
-      O = fmax(O, fabs(so[j]));
-    }
-    const double m = ((double)extent + O) * 0x1p-20;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double a = -(so[j] * iv[j]), dl = iv[j] > 0.0 ? m * iv[j] : -(m * iv[j]);
-      const double sdl = iv[j] > 0.0 ? dl : -dl;
-      s.inv32[j] = (float)iv[j];
-      s.c32[2 * j] = (float)(a - sdl);
-      s.c32[2 * j + 1] = (float)(a + sdl);
-    }
-    s.flags = (ok ? 1u : 0u) | (ray_octant(sdir) << 1);
+    g0 = coop_stage(M, aux != nullptr, r, tmin32, tmax_in);
+    walk = g0.walk;
   }
+  uint64_t act = __ballot(walk);
+  uint32_t n0 = (uint32_t)__popcll(act), n = n0;  // n: pool entries so far (PAIR: grows)
+  uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  if (walk) {
+    coop_write(rays[PAIR ? lane : rank], r, tmax_in, g0);
+    if (PAIR) order[rank] = (uint8_t)lane;
+  }
+  if (PAIR && pair) {  // a ray the first instance's cull box rejects goes straight to the second
+    const bool miss0 = want && !walk;
+    CoopStage g1{};
+    if (miss0) {
+      const Ray rr = r1();
+      g1 = coop_stage(M, aux != nullptr, rr, tmin32, tmax_in);
+      walk1 = g1.walk;
+      if (walk1) coop_write(rays[lane], rr, tmax_in, g1);
+    }
+    const uint64_t a1 = __ballot(walk1);
+    if (walk1) order[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u))] = (uint8_t)lane;
+    n += (uint32_t)__popcll(a1);
+  }
+  if (n == 0) return;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
-  uint32_t ray = q, next = 16;
+  uint32_t ray = q, next = 16, slot = 0;  // slot: the record of the quad's ray
+  uint32_t pend = 0;  // PAIR: first-instance walks finished whose lanes have not formed their second record
+  // PAIR, per lane: the first instance's answer, kept from the moment the record is reused
+  // (only the triangle in a VGPR: t is the second record's t_max, u and v are formed again from
+  // the triangle, and the exact check of the first answer is made when it is saved)
+  bool f0 = false, done0 = false, redo0 = false;
+  uint32_t tri0 = 0;
+  const bool force = __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+  static_assert(!PAIR || (YART_COOP_POSTCHECK && SLOTS == kCoopSlots), "PAIR walks check their answers after the walk");
   // YART_COOP_POSTCHECK: W's exact check after the walk, per lane (the 32-slot walks only: the
   // per-lane re-walk, qbvh_t, has a 32-slot stack)
   constexpr bool kPostCheck = YART_COOP_POSTCHECK && SLOTS == kCoopSlots;
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
   double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
-  const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
   float inv32[3], teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
@@ -1069,7 +1193,8 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     f2b = front_to_back;
   };
   auto take = [&]() {
-    const CoopRay& s = rays[ray];
+    slot = PAIR ? (uint32_t)order[ray] : ray;
+    const CoopRay& s = rays[slot];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       ro[j] = s.o[j]; rd[j] = s.d[j];
@@ -1084,11 +1209,44 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   if (ray < n) take();
   if (STATS && lane == 0) st.v[ST_WALKS]++;
   for (;;) {
+    if (PAIR && pend != 0 && next >= n) {  // wave-uniform: the pool is empty, second records wait
+      // Every lane whose first-instance walk has finished saves that answer and forms its second
+      // record in place, t_max = the answer (the list walk's closest so far); the quads without a
+      // ray take the new entries.
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const bool cand = walk && !done0 && (rays[lane].flags & kCoopDone) != 0u;
+      bool add = false;
+      if (cand) {
+        done0 = true;
+        add = coop_restage(rays[lane], M, aux, r, tmin, tmin32, tmax_in, force, f0, tri0, redo0, r1);
+      }
+      const uint64_t am = __ballot(add);
+      pend = 0;  // every finished first walk has its second record now (or none: culled)
+      if (add) {
+        walk1 = true;
+        order[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] = (uint8_t)lane;
+      }
+      const uint32_t base = n;
+      n += (uint32_t)__popcll(am);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint64_t idle = __ballot(ray >= base && c == 0);  // quads without a ray (ray >= base)
+      if (ray >= base) {
+        ray = base + (uint32_t)__popcll(idle & ((1ull << (4u * q)) - 1ull));
+        if (ray < n) take();
+      }
+      next = base + (uint32_t)__popcll(idle);
+    }
     const bool has = ray < n;
-    if (__ballot(has) == 0) break;
-    if (STATS && lane == 0) {
-      st.v[ST_ROUNDS]++;
-      st.v[ST_LEAF_ROUNDS] += __ballot(has && (node >> 31)) != 0 ? 1u : 0u;
+    if (__ballot(has) == 0) {
+      if (!PAIR || pend == 0 || next < n) break;  // (next < n with every quad idle cannot happen)
+      continue;
+    }
+    if (STATS) {  // the ballot outside the lane-0 branch: it must see every quad
+      const bool any_leaf = __ballot(has && (node >> 31)) != 0;
+      if (lane == 0) {
+        st.v[ST_ROUNDS]++;
+        st.v[ST_LEAF_ROUNDS] += any_leaf ? 1u : 0u;
+      }
     }
     bool fin = false;
 #if YART_COOP_LEAF_MIN > 1
@@ -1143,7 +1301,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           if (better) {
             tb = t; fnd = true; bleaf = li; bkey = key;
             if (c == w) {
-              CoopRay& s = rays[ray];
+              CoopRay& s = rays[slot];
               s.o[0] = t; s.o[1] = u; s.o[2] = v;
               s.d[0] = __longlong_as_double((long long)((1ull << 32) | id));
             }
@@ -1223,7 +1381,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
         }
       }
       if (kPostCheck && fin && c == 0)  // the ray's own lane checks W after the walk (below)
-        rays[ray].flags = (f2b && fnd) ? (0x80000000u | bleaf) : 0u;
+        rays[slot].flags = (PAIR ? kCoopDone : 0u) | ((f2b && fnd) ? (0x80000000u | bleaf) : 0u);
       if (!kPostCheck && fin && f2b && fnd) {
         // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
         // (the f32 test visits a superset) and W's t is not before that box's entry (above)
@@ -1243,8 +1401,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
         }
       }
     }
-    if (fin && !fnd && c == 0) rays[ray].d[0] = 0.0;  // no hit (a hit's record is already written)
+    if (fin && !fnd && c == 0) rays[slot].d[0] = 0.0;  // no hit (a hit's record is already written)
     const uint64_t fm = __ballot(fin && c == 0);
+    if (PAIR && pair && fm) pend += (uint32_t)__popcll(__ballot(fin && c == 0 && ray < n0));  // first-instance entries
     if (fm) {
       if (fin) {
         ray = next + (uint32_t)__popcll(fm & ((1ull << (4u * q)) - 1ull));
@@ -1254,38 +1413,85 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  bool redo = false;
-  if (want) {
-    const CoopRay& s = rays[rank];
-    const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
-    found = (res >> 32) != 0;
-    t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
-    tri = (uint32_t)res;
-    const uint32_t fl = s.flags;
-    if (kPostCheck && (fl >> 31)) {
-      // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
-      // (the f32 test visits a superset) and W's t is not before that box's entry (above): each
-      // lane checks its own ray once, after the walk, instead of the whole wave at every ray's end.
-      const auto& A = aux[fl & 0x7FFFFFFFu];
-      const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
-      double l = tmin, h = tmax_in;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double iv = 1.0 / rd[j];
-        const double t0 = ((double)A.lo[j] - ro[j]) * iv, t1 = ((double)A.hi[j] - ro[j]) * iv;
-        l = fmax(l, fmin(t0, t1));
-        h = fmin(h, fmax(t0, t1));
-      }
-      redo = !(h > l && t_hit >= l) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+  // W is the reference's answer if its leaf box passes the reference's f64 test at the walk's
+  // t_max (the f32 test visits a superset) and W's t is not before that box's entry (above): each
+  // lane checks its own ray once, after the walk, instead of the whole wave at every ray's end. A
+  // ray that fails walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in this
+  // wave's LDS, free once every lane has read its record) — rare.
+  uint32_t* const lane_stk = reinterpret_cast<uint32_t*>(lds) + lane;
+  if constexpr (!PAIR) {
+    bool redo = false;
+    if (walk) {
+      const CoopRay& s = rays[rank];
+      const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
+      found = (res >> 32) != 0;
+      t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
+      tri = (uint32_t)res;
+      const uint32_t fl = s.flags;
+      if (kPostCheck && (fl >> 31)) redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || force;
     }
-  }
-  if (kPostCheck && __ballot(redo) != 0ull) {
-    // Rare: that ray walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in
-    // this wave's LDS, free now that every lane has read its record).
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (redo) {
-      if (STATS) st.v[ST_REWALK]++;
-      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
+    if (kPostCheck && __ballot(redo) != 0ull) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (redo) {
+        if (STATS) st.v[ST_REWALK]++;
+        found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, lane_stk, st);
+      }
+    }
+  } else {
+    // The lane's record holds the second walk's answer (walk1; its t_max is the first answer's t)
+    // or else the first walk's (no second walk: culled, after a failed check, or a single instance).
+    bool f1 = false;
+    double t0 = 0.0, u0 = 0.0, v0 = 0.0, t1 = 0.0, u1 = 0.0, v1 = 0.0;
+    uint32_t tri1 = 0, fl1 = 0;
+    if (walk || walk1) {
+      const CoopRay& s = rays[lane];
+      const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
+      if (walk1) {
+        f1 = (res >> 32) != 0;
+        t1 = s.o[0]; u1 = s.o[1]; v1 = s.o[2];
+        tri1 = (uint32_t)res;
+        fl1 = s.flags;
+        t0 = s.tmax;
+      } else {
+        t0 = s.o[0]; u0 = s.o[1]; v0 = s.o[2];
+        if (!done0) {  // a single instance: its answer is checked here
+          f0 = (res >> 32) != 0;
+          tri0 = (uint32_t)res;
+          const uint32_t fl = s.flags;
+          redo0 = (fl >> 31) && (!coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t0) || force);
+        }
+      }
+    }
+    if (__ballot(redo0) != 0ull) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (redo0) {
+        if (STATS) st.v[ST_REWALK]++;
+        f0 = qbvh_t<STATS>(M, r, tmin, tmax_in, t0, tri0, u0, v0, lane_stk, st);
+      }
+    }
+    // the second walk's t_max is the first answer: after a re-walk of the first, it walks now
+    const double c0 = f0 ? t0 : tmax_in;
+    bool redo1 = pair && redo0;
+    if (pair && !redo0 && walk1 && (fl1 >> 31)) redo1 = !coop_check(aux, fl1 & 0x3FFFFFFFu, r1(), tmin, c0, t1) || force;
+    if (__ballot(redo1) != 0ull) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (redo1) {
+        if (STATS) st.v[ST_REWALK]++;
+        f1 = qbvh_t<STATS>(M, r1(), tmin, c0, t1, tri1, u1, v1, lane_stk, st);
+      }
+    }
+    if (f1) {  // strictly nearer than the first instance's answer (its t_max)
+      found = true; t_hit = t1; u_hit = u1; v_hit = v1; tri = tri1; *inst = 1u;
+    } else if (f0) {
+      if (walk1) {
+        // the second walk took the record over: u and v of the first answer formed again from its
+        // triangle (record tri0 of the sorted order) and ray — the walk's arithmetic, so its values
+        const gfloat4p R = leaves + 3 * (size_t)tri0;
+        const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+        double tt;
+        leaf_tri_hit(ld4(R, 0), ld4(R, 1), ld4(R, 2), ro, rd, tmin, INFINITY, tt, u0, v0);
+      }
+      found = true; t_hit = t0; u_hit = u0; v_hit = v0; tri = tri0; *inst = 0u;
     }
   }
 }
@@ -1428,6 +1634,27 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
+#if YART_COOP_PAIR
+      if constexpr (SLOTS == kCoopSlots && YART_COOP_POSTCHECK) {
+        // the next entry another instance of the same mesh (david's two statues): one shared pool
+        // (the pooled walk with pair = false is the single walk: one inlined copy either way)
+        const uint32_t i1 = i + 1 < S.n_objects ? i + 1 : i;
+        const DevObject& o1 = uniform_at(S.objects, i1);
+        const uint32_t nxf1 = o1.n_xf;
+        const bool pair = i1 != i && o1.kind == YART_PRIM_MESH && o1.mesh == o.mesh &&
+                          !(EXT && nxf1 != 0 && o1.xf_kind[0] == YART_XF_MEDIUM);
+        uint32_t inst = 0;
+        qbvh_coop<STATS, SLOTS, true>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st,
+                                      &inst, pair, [&]() { return to_local(uniform_at(S.objects, i1), nxf1, r); });
+        if (hit) {
+          closest = t;
+          id.obj = i + inst; id.sub = sub; id.u = u; id.v = v;
+          found = true;
+        }
+        if (pair) ++i;
+        continue;
+      }
+#endif
       qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
       if (hit) {
         closest = t;
