@@ -900,13 +900,8 @@ constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
 constexpr int kCoopSlots = kStackSlots;
 constexpr int kDeepSlots = kMaxStackSlots;
 template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS * 16 * (4 + (int)sizeof(CoopEnt)); }
-#ifndef YART_COOP_PAIR
-#define YART_COOP_PAIR 0  // two consecutive instances of one mesh in one walk pool: measured slower
-#endif
-constexpr int kCoopOrderBytes = YART_COOP_PAIR ? 128 : 0;  // a paired walk's hand-out order, after the stacks
 template <int SLOTS> constexpr int wave_lds_words() {
-  return ((coop_bytes<SLOTS>() + kCoopOrderBytes) / 4 > kStackSlots * 64) ? (coop_bytes<SLOTS>() + kCoopOrderBytes) / 4
-                                                                          : kStackSlots * 64;
+  return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
 }
 constexpr int kCoopBytes = coop_bytes<kCoopSlots>();
 // LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
@@ -981,6 +976,13 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 #endif
 #ifndef YART_COOP_CULL
 #define YART_COOP_CULL 1  // rays missing the mesh's cull box stay out of the walk (qbvh_coop)
+#endif
+#ifndef YART_COOP_SPEC
+#define YART_COOP_SPEC 0  // > 0: parked leaves, a leaf round once this many quads wait (qbvh_coop)
+#endif
+constexpr uint32_t kCoopSent = 0x7FFFFFFFu;  // YART_COOP_SPEC: no node left (not a leaf, not an index)
+#ifndef YART_COOP_PRIO
+#define YART_COOP_PRIO 0  // pool order by the caller's hint (k_render: 1 glass-scattered rays first, 2 secondary)
 #endif
 // Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
 // reference's order, so the rare path is exercised on whole frames.
@@ -1075,55 +1077,16 @@ __device__ __forceinline__ bool coop_check(const __attribute__((address_space(1)
   }
   return h > l && t >= l;
 }
-// PAIR: a lane whose first walk has finished saves that answer (the triangle, whether it hit, and
-// its exact check, made now) and forms its second record in place with t_max = the first answer.
-// Out of line: the pool reaches it a few times per walk, and inlined its temporaries crowded the
-// walk loop's registers.
-template <class R1>
-__device__ __noinline__ bool coop_restage(CoopRay& s, const DevMesh& M, const __attribute__((address_space(1))) LeafAux* aux,
-                                          const Ray& r, double tmin, float tmin32, double tmax_in, bool force, bool& f0,
-                                          uint32_t& tri0, bool& redo0, R1 r1);
-struct NoSecond { __device__ Ray operator()() const { return Ray{}; } };
-constexpr uint32_t kCoopDone = 0x40000000u;  // PAIR: a record's flags once its walk has finished
-template <class R1>
-__device__ __noinline__ bool coop_restage(CoopRay& s, const DevMesh& M, const __attribute__((address_space(1))) LeafAux* aux,
-                                          const Ray& r, double tmin, float tmin32, double tmax_in, bool force, bool& f0,
-                                          uint32_t& tri0, bool& redo0, R1 r1) {
-  const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
-  f0 = (res >> 32) != 0;
-  const double t0 = s.o[0];
-  tri0 = (uint32_t)res;
-  const uint32_t fl = s.flags;  // kCoopDone | the post-check request
-  redo0 = (fl >> 31) && (!coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t0) || force);
-  if (redo0) return false;  // walked again after the pool, and the second instance with it
-  const double c0 = f0 ? t0 : tmax_in;
-  const Ray rr = r1();
-  const CoopStage g1 = coop_stage(M, aux != nullptr, rr, tmin32, c0);
-  // the record keeps the first answer (o, d[0]) unless the second walk takes it over
-  if (g1.walk) coop_write(s, rr, c0, g1);
-  return g1.walk;
-}
-
-// PAIR (two consecutive list entries holding the same mesh, e.g. david's two statues,
-// scenes.rs:581-596): both walks share one pool. Entries of the second instance join it as the
-// first instance's walks finish — a finished ray's lane forms its second record (r1(): the ray in
-// the second instance's frame) with t_max = the first instance's answer, exactly the t_max the
-// list walk (hittable.rs:67-79) passes on — so the pool does not drain twice. Records are then
-// indexed by lane, and the pool's order is a byte list per wave after the stacks. The answer is
-// the list walk's: the second instance's hit if it has one (it is strictly nearer by its t_max),
-// else the first's; `inst` says which.
-template <bool STATS, int SLOTS = kCoopSlots, bool PAIR = false, class R1 = NoSecond>
+template <bool STATS, int SLOTS = kCoopSlots>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
-                                       uint8_t* __restrict__ lds, Stats& st, uint32_t* inst = nullptr, bool pair = false, R1 r1 = R1()) {
+                                       uint8_t* __restrict__ lds, Stats& st, bool prio = false) {
   found = false;
-  if (PAIR) *inst = 0u;
   if (__ballot(want) == 0) return;
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
   CoopEnt* qent = reinterpret_cast<CoopEnt*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
-  uint8_t* order = lds + coop_bytes<SLOTS>();  // PAIR: the pool's records in hand-out order
   // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
@@ -1131,44 +1094,29 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   const uint32_t root = M.root, wroot = M.wroot;  // reference tree / walk tree (front to back)
   const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
   // Each lane forms its own ray's record before the pool is laid out (coop_stage).
-  bool walk = false, walk1 = false;  // PAIR: walk1 = the second instance's record is in the pool
+  bool walk = false;
   CoopStage g0{};
   if (want) {
     g0 = coop_stage(M, aux != nullptr, r, tmin32, tmax_in);
     walk = g0.walk;
   }
   uint64_t act = __ballot(walk);
-  uint32_t n0 = (uint32_t)__popcll(act), n = n0;  // n: pool entries so far (PAIR: grows)
+  const uint32_t n = (uint32_t)__popcll(act);
   uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  if (walk) {
-    coop_write(rays[PAIR ? lane : rank], r, tmax_in, g0);
-    if (PAIR) order[rank] = (uint8_t)lane;
+#if YART_COOP_PRIO
+  {  // the rays the caller expects to walk longest are handed out first, so they do not start late
+    const uint64_t ahi = __ballot(walk && prio), alo = act & ~ahi;
+    rank = prio ? __builtin_amdgcn_mbcnt_hi((uint32_t)(ahi >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ahi, 0u))
+                : (uint32_t)__popcll(ahi) + __builtin_amdgcn_mbcnt_hi((uint32_t)(alo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)alo, 0u));
   }
-  if (PAIR && pair) {  // a ray the first instance's cull box rejects goes straight to the second
-    const bool miss0 = want && !walk;
-    CoopStage g1{};
-    if (miss0) {
-      const Ray rr = r1();
-      g1 = coop_stage(M, aux != nullptr, rr, tmin32, tmax_in);
-      walk1 = g1.walk;
-      if (walk1) coop_write(rays[lane], rr, tmax_in, g1);
-    }
-    const uint64_t a1 = __ballot(walk1);
-    if (walk1) order[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u))] = (uint8_t)lane;
-    n += (uint32_t)__popcll(a1);
+#endif
+  if (walk) {
+    coop_write(rays[rank], r, tmax_in, g0);
   }
   if (n == 0) return;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
-  uint32_t ray = q, next = 16, slot = 0;  // slot: the record of the quad's ray
-  uint32_t pend = 0;  // PAIR: first-instance walks finished whose lanes have not formed their second record
-  // PAIR, per lane: the first instance's answer, kept from the moment the record is reused
-  // (only the triangle in a VGPR: t is the second record's t_max, u and v are formed again from
-  // the triangle, and the exact check of the first answer is made when it is saved)
-  bool f0 = false, done0 = false, redo0 = false;
-  uint32_t tri0 = 0;
-  const bool force = __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
-  static_assert(!PAIR || (YART_COOP_POSTCHECK && SLOTS == kCoopSlots), "PAIR walks check their answers after the walk");
+  uint32_t ray = q, next = 16;
   // YART_COOP_POSTCHECK: W's exact check after the walk, per lane (the 32-slot walks only: the
   // per-lane re-walk, qbvh_t, has a 32-slot stack)
   constexpr bool kPostCheck = YART_COOP_POSTCHECK && SLOTS == kCoopSlots;
@@ -1179,10 +1127,12 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
   uint32_t pos = 0, node = 0, bleaf = 0, bkey = 0;
+  uint32_t pl = 0;  // YART_COOP_SPEC: a leaf reached front to back, parked until a leaf round
   int cursor = 0;
   bool fnd = false, f2b = false;
   auto restart = [&](bool front_to_back) {
     node = front_to_back ? wroot : root;
+    pl = 0;
     bkey = 0xFFFFFFFFu;
     cursor = 0;
     fnd = false;
@@ -1193,8 +1143,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     f2b = front_to_back;
   };
   auto take = [&]() {
-    slot = PAIR ? (uint32_t)order[ray] : ray;
-    const CoopRay& s = rays[slot];
+    const CoopRay& s = rays[ray];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       ro[j] = s.o[j]; rd[j] = s.d[j];
@@ -1209,38 +1158,8 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   if (ray < n) take();
   if (STATS && lane == 0) st.v[ST_WALKS]++;
   for (;;) {
-    if (PAIR && pend != 0 && next >= n) {  // wave-uniform: the pool is empty, second records wait
-      // Every lane whose first-instance walk has finished saves that answer and forms its second
-      // record in place, t_max = the answer (the list walk's closest so far); the quads without a
-      // ray take the new entries.
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const bool cand = walk && !done0 && (rays[lane].flags & kCoopDone) != 0u;
-      bool add = false;
-      if (cand) {
-        done0 = true;
-        add = coop_restage(rays[lane], M, aux, r, tmin, tmin32, tmax_in, force, f0, tri0, redo0, r1);
-      }
-      const uint64_t am = __ballot(add);
-      pend = 0;  // every finished first walk has its second record now (or none: culled)
-      if (add) {
-        walk1 = true;
-        order[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] = (uint8_t)lane;
-      }
-      const uint32_t base = n;
-      n += (uint32_t)__popcll(am);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const uint64_t idle = __ballot(ray >= base && c == 0);  // quads without a ray (ray >= base)
-      if (ray >= base) {
-        ray = base + (uint32_t)__popcll(idle & ((1ull << (4u * q)) - 1ull));
-        if (ray < n) take();
-      }
-      next = base + (uint32_t)__popcll(idle);
-    }
     const bool has = ray < n;
-    if (__ballot(has) == 0) {
-      if (!PAIR || pend == 0 || next < n) break;  // (next < n with every quad idle cannot happen)
-      continue;
-    }
+    if (__ballot(has) == 0) break;
     if (STATS) {  // the ballot outside the lane-0 branch: it must see every quad
       const bool any_leaf = __ballot(has && (node >> 31)) != 0;
       if (lane == 0) {
@@ -1249,6 +1168,24 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
       }
     }
     bool fin = false;
+#if YART_COOP_SPEC
+    // Speculative leaf postponing (Aila & Laine's postponed leaves, on quads): a quad that reaches
+    // a leaf front to back parks it (one slot) and keeps descending, so the wave runs the leaf
+    // branch once for many quads instead of in nearly every round. A quad that cannot step — a
+    // second leaf while one is parked, or its stack done with one parked — waits for a leaf
+    // round, which comes when YART_COOP_SPEC quads wait or no quad can step. The answer is the
+    // minimum over the tested candidates under (t, key), whatever order they are tested in, and
+    // the pruning bound only ever lags the best so far (the walk tests a superset).
+    const bool io = has && node != kCoopSent && !(node >> 31);
+    const bool lwork = has && (pl != 0u || (node >> 31));
+    const bool leaf_round = __popcll(__ballot(has && !io && c == 0)) >= YART_COOP_SPEC || __ballot(io) == 0;
+    const bool do_leaf = leaf_round && lwork;
+    const uint32_t cur = do_leaf && pl != 0u ? pl : node;  // the leaf to test, or the inner node
+    if (do_leaf || io) {  // quad-uniform from here on
+      bool popped = false;
+      if (do_leaf) {
+        const uint32_t lnode = cur;
+#else
 #if YART_COOP_LEAF_MIN > 1
     // Leaf rounds wait until enough quads sit at a leaf (or none can descend): a round pays for
     // each branch any quad takes, and the leaf branch is the expensive one.
@@ -1261,8 +1198,10 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
       bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
-        uint32_t count = (node >> 27) & 0xFu;
-        const uint32_t first = node & ((1u << 27) - 1u);
+        const uint32_t lnode = node;
+#endif
+        uint32_t count = (lnode >> 27) & 0xFu;
+        const uint32_t first = lnode & ((1u << 27) - 1u);
 #ifdef YART_WALK_CHECK
         if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
 #endif
@@ -1301,7 +1240,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
           if (better) {
             tb = t; fnd = true; bleaf = li; bkey = key;
             if (c == w) {
-              CoopRay& s = rays[slot];
+              CoopRay& s = rays[ray];
               s.o[0] = t; s.o[1] = u; s.o[2] = v;
               s.d[0] = __longlong_as_double((long long)((1ull << 32) | id));
             }
@@ -1315,6 +1254,12 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
             }
           }
         }
+#if YART_COOP_SPEC
+        if (pl != 0u) {  // the parked leaf was tested: a leaf at `node` takes its place, else `node` stays
+          pl = (node >> 31) ? node : 0u;
+          popped = !(node >> 31);
+        }
+#endif
       } else {
 #ifdef YART_WALK_CHECK
         if (node >= M.n_nodes) { walk_fault(4u); node = root; }
@@ -1370,18 +1315,33 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
 #endif
           node = nx;
           popped = true;
+#if YART_COOP_SPEC
+          if (f2b && (nx >> 31) && pl == 0u) { pl = nx; popped = false; }  // park it, take the next entry
+#endif
         }
       }
       if (!popped) {
         for (;;) {  // front to back: entries whose box begins beyond the bound are dropped
+#if YART_COOP_SPEC
+          if (cursor == 0) { node = kCoopSent; break; }
+          cursor -= 1;
+          node = qstk[cursor * 16 + (int)q];
+          if (f2b && __uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound) continue;
+          if (f2b && (node >> 31) && pl == 0u) { pl = node; continue; }  // park the first leaf
+          break;
+#else
           if (cursor == 0) { fin = true; break; }
           cursor -= 1;
           node = qstk[cursor * 16 + (int)q];
           if (!f2b || !(__uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound)) break;
+#endif
         }
       }
+#if YART_COOP_SPEC
+      fin = node == kCoopSent && pl == 0u;
+#endif
       if (kPostCheck && fin && c == 0)  // the ray's own lane checks W after the walk (below)
-        rays[slot].flags = (PAIR ? kCoopDone : 0u) | ((f2b && fnd) ? (0x80000000u | bleaf) : 0u);
+        rays[ray].flags = (f2b && fnd) ? (0x80000000u | bleaf) : 0u;
       if (!kPostCheck && fin && f2b && fnd) {
         // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
         // (the f32 test visits a superset) and W's t is not before that box's entry (above)
@@ -1401,9 +1361,8 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
         }
       }
     }
-    if (fin && !fnd && c == 0) rays[slot].d[0] = 0.0;  // no hit (a hit's record is already written)
+    if (fin && !fnd && c == 0) rays[ray].d[0] = 0.0;  // no hit (a hit's record is already written)
     const uint64_t fm = __ballot(fin && c == 0);
-    if (PAIR && pair && fm) pend += (uint32_t)__popcll(__ballot(fin && c == 0 && ray < n0));  // first-instance entries
     if (fm) {
       if (fin) {
         ray = next + (uint32_t)__popcll(fm & ((1ull << (4u * q)) - 1ull));
@@ -1419,79 +1378,22 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   // ray that fails walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in this
   // wave's LDS, free once every lane has read its record) — rare.
   uint32_t* const lane_stk = reinterpret_cast<uint32_t*>(lds) + lane;
-  if constexpr (!PAIR) {
-    bool redo = false;
-    if (walk) {
-      const CoopRay& s = rays[rank];
-      const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
-      found = (res >> 32) != 0;
-      t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
-      tri = (uint32_t)res;
-      const uint32_t fl = s.flags;
-      if (kPostCheck && (fl >> 31)) redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || force;
-    }
-    if (kPostCheck && __ballot(redo) != 0ull) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (redo) {
-        if (STATS) st.v[ST_REWALK]++;
-        found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, lane_stk, st);
-      }
-    }
-  } else {
-    // The lane's record holds the second walk's answer (walk1; its t_max is the first answer's t)
-    // or else the first walk's (no second walk: culled, after a failed check, or a single instance).
-    bool f1 = false;
-    double t0 = 0.0, u0 = 0.0, v0 = 0.0, t1 = 0.0, u1 = 0.0, v1 = 0.0;
-    uint32_t tri1 = 0, fl1 = 0;
-    if (walk || walk1) {
-      const CoopRay& s = rays[lane];
-      const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
-      if (walk1) {
-        f1 = (res >> 32) != 0;
-        t1 = s.o[0]; u1 = s.o[1]; v1 = s.o[2];
-        tri1 = (uint32_t)res;
-        fl1 = s.flags;
-        t0 = s.tmax;
-      } else {
-        t0 = s.o[0]; u0 = s.o[1]; v0 = s.o[2];
-        if (!done0) {  // a single instance: its answer is checked here
-          f0 = (res >> 32) != 0;
-          tri0 = (uint32_t)res;
-          const uint32_t fl = s.flags;
-          redo0 = (fl >> 31) && (!coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t0) || force);
-        }
-      }
-    }
-    if (__ballot(redo0) != 0ull) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (redo0) {
-        if (STATS) st.v[ST_REWALK]++;
-        f0 = qbvh_t<STATS>(M, r, tmin, tmax_in, t0, tri0, u0, v0, lane_stk, st);
-      }
-    }
-    // the second walk's t_max is the first answer: after a re-walk of the first, it walks now
-    const double c0 = f0 ? t0 : tmax_in;
-    bool redo1 = pair && redo0;
-    if (pair && !redo0 && walk1 && (fl1 >> 31)) redo1 = !coop_check(aux, fl1 & 0x3FFFFFFFu, r1(), tmin, c0, t1) || force;
-    if (__ballot(redo1) != 0ull) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (redo1) {
-        if (STATS) st.v[ST_REWALK]++;
-        f1 = qbvh_t<STATS>(M, r1(), tmin, c0, t1, tri1, u1, v1, lane_stk, st);
-      }
-    }
-    if (f1) {  // strictly nearer than the first instance's answer (its t_max)
-      found = true; t_hit = t1; u_hit = u1; v_hit = v1; tri = tri1; *inst = 1u;
-    } else if (f0) {
-      if (walk1) {
-        // the second walk took the record over: u and v of the first answer formed again from its
-        // triangle (record tri0 of the sorted order) and ray — the walk's arithmetic, so its values
-        const gfloat4p R = leaves + 3 * (size_t)tri0;
-        const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
-        double tt;
-        leaf_tri_hit(ld4(R, 0), ld4(R, 1), ld4(R, 2), ro, rd, tmin, INFINITY, tt, u0, v0);
-      }
-      found = true; t_hit = t0; u_hit = u0; v_hit = v0; tri = tri0; *inst = 0u;
+  const bool force = __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+  bool redo = false;
+  if (walk) {
+    const CoopRay& s = rays[rank];
+    const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
+    found = (res >> 32) != 0;
+    t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
+    tri = (uint32_t)res;
+    const uint32_t fl = s.flags;
+    if (kPostCheck && (fl >> 31)) redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || force;
+  }
+  if (kPostCheck && __ballot(redo) != 0ull) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (redo) {
+      if (STATS) st.v[ST_REWALK]++;
+      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, lane_stk, st);
     }
   }
 }
@@ -1621,7 +1523,7 @@ __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
 template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                              LightCap* cap = nullptr) {
+                                              LightCap* cap = nullptr, bool prio = false) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -1634,28 +1536,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-#if YART_COOP_PAIR
-      if constexpr (SLOTS == kCoopSlots && YART_COOP_POSTCHECK) {
-        // the next entry another instance of the same mesh (david's two statues): one shared pool
-        // (the pooled walk with pair = false is the single walk: one inlined copy either way)
-        const uint32_t i1 = i + 1 < S.n_objects ? i + 1 : i;
-        const DevObject& o1 = uniform_at(S.objects, i1);
-        const uint32_t nxf1 = o1.n_xf;
-        const bool pair = i1 != i && o1.kind == YART_PRIM_MESH && o1.mesh == o.mesh &&
-                          !(EXT && nxf1 != 0 && o1.xf_kind[0] == YART_XF_MEDIUM);
-        uint32_t inst = 0;
-        qbvh_coop<STATS, SLOTS, true>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st,
-                                      &inst, pair, [&]() { return to_local(uniform_at(S.objects, i1), nxf1, r); });
-        if (hit) {
-          closest = t;
-          id.obj = i + inst; id.sub = sub; id.u = u; id.v = v;
-          found = true;
-        }
-        if (pair) ++i;
-        continue;
-      }
-#endif
-      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
+      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st, prio);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1856,12 +1737,12 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
 template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
                                           int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                          LightCap* cap = nullptr) {
+                                          LightCap* cap = nullptr, bool prio = false) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap, prio) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -2480,7 +2361,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
     if (__ballot(run) == 0) break;
     double R = 0.0;
-    bool term = false, want = false;
+    bool term = false, want = false, sec = false;  // sec: this iteration scattered (not a camera ray)
     // LPF: a Lambertian scatter's mixture pdf waits for the world pass of the ray it sampled,
     // which captures the light hits pdf_value would re-test (device_types.h kMaxLpf): T·att·spdf
     // (Tp) and the cosine half (cosv) are kept until then, T stays the incoming throughput.
@@ -2563,6 +2444,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         fresh = false;
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
         PROF(PF_SCATTER);
+        sec = true;
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
         auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
@@ -2618,7 +2500,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         PROF(PF_WORLD);
         DUP_LOOP(3) {
         DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+        bool prio = false;  // YART_COOP_PRIO: rays expected to walk long go first in the mesh walk's pool
+#if YART_COOP_PRIO == 1
+        prio = sec && S.materials[hmat].kind == YART_MAT_DIELECTRIC;  // inside or into glass
+#elif YART_COOP_PRIO == 2
+        prio = sec;  // every secondary ray
+#endif
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q, nullptr, prio);
         DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
         }
       } else if (want) {
