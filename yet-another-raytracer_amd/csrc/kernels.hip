@@ -903,7 +903,6 @@ template <int SLOTS> constexpr int coop_bytes() { return kCoopRayBytes + SLOTS *
 template <int SLOTS> constexpr int wave_lds_words() {
   return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
 }
-constexpr int kCoopBytes = coop_bytes<kCoopSlots>();
 // LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
 constexpr int kWaveLdsWords = wave_lds_words<kCoopSlots>();
 constexpr double kF2bMargin = 0x1p-8;
@@ -976,13 +975,6 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 #endif
 #ifndef YART_COOP_CULL
 #define YART_COOP_CULL 1  // rays missing the mesh's cull box stay out of the walk (qbvh_coop)
-#endif
-#ifndef YART_COOP_SPEC
-#define YART_COOP_SPEC 0  // > 0: parked leaves, a leaf round once this many quads wait (qbvh_coop)
-#endif
-constexpr uint32_t kCoopSent = 0x7FFFFFFFu;  // YART_COOP_SPEC: no node left (not a leaf, not an index)
-#ifndef YART_COOP_PRIO
-#define YART_COOP_PRIO 0  // pool order by the caller's hint (k_render: 1 glass-scattered rays first, 2 secondary)
 #endif
 // Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
 // reference's order, so the rare path is exercised on whole frames.
@@ -1080,7 +1072,7 @@ __device__ __forceinline__ bool coop_check(const __attribute__((address_space(1)
 template <bool STATS, int SLOTS = kCoopSlots>
 __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
-                                       uint8_t* __restrict__ lds, Stats& st, bool prio = false) {
+                                       uint8_t* __restrict__ lds, Stats& st) {
   found = false;
   if (__ballot(want) == 0) return;
   const uint32_t lane = __lane_id();
@@ -1102,14 +1094,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   }
   uint64_t act = __ballot(walk);
   const uint32_t n = (uint32_t)__popcll(act);
-  uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-#if YART_COOP_PRIO
-  {  // the rays the caller expects to walk longest are handed out first, so they do not start late
-    const uint64_t ahi = __ballot(walk && prio), alo = act & ~ahi;
-    rank = prio ? __builtin_amdgcn_mbcnt_hi((uint32_t)(ahi >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ahi, 0u))
-                : (uint32_t)__popcll(ahi) + __builtin_amdgcn_mbcnt_hi((uint32_t)(alo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)alo, 0u));
-  }
-#endif
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
   if (walk) {
     coop_write(rays[rank], r, tmax_in, g0);
   }
@@ -1127,12 +1112,10 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
   uint32_t pos = 0, node = 0, bleaf = 0, bkey = 0;
-  uint32_t pl = 0;  // YART_COOP_SPEC: a leaf reached front to back, parked until a leaf round
   int cursor = 0;
   bool fnd = false, f2b = false;
   auto restart = [&](bool front_to_back) {
     node = front_to_back ? wroot : root;
-    pl = 0;
     bkey = 0xFFFFFFFFu;
     cursor = 0;
     fnd = false;
@@ -1168,24 +1151,6 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
       }
     }
     bool fin = false;
-#if YART_COOP_SPEC
-    // Speculative leaf postponing (Aila & Laine's postponed leaves, on quads): a quad that reaches
-    // a leaf front to back parks it (one slot) and keeps descending, so the wave runs the leaf
-    // branch once for many quads instead of in nearly every round. A quad that cannot step — a
-    // second leaf while one is parked, or its stack done with one parked — waits for a leaf
-    // round, which comes when YART_COOP_SPEC quads wait or no quad can step. The answer is the
-    // minimum over the tested candidates under (t, key), whatever order they are tested in, and
-    // the pruning bound only ever lags the best so far (the walk tests a superset).
-    const bool io = has && node != kCoopSent && !(node >> 31);
-    const bool lwork = has && (pl != 0u || (node >> 31));
-    const bool leaf_round = __popcll(__ballot(has && !io && c == 0)) >= YART_COOP_SPEC || __ballot(io) == 0;
-    const bool do_leaf = leaf_round && lwork;
-    const uint32_t cur = do_leaf && pl != 0u ? pl : node;  // the leaf to test, or the inner node
-    if (do_leaf || io) {  // quad-uniform from here on
-      bool popped = false;
-      if (do_leaf) {
-        const uint32_t lnode = cur;
-#else
 #if YART_COOP_LEAF_MIN > 1
     // Leaf rounds wait until enough quads sit at a leaf (or none can descend): a round pays for
     // each branch any quad takes, and the leaf branch is the expensive one.
@@ -1198,10 +1163,8 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
       bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
-        const uint32_t lnode = node;
-#endif
-        uint32_t count = (lnode >> 27) & 0xFu;
-        const uint32_t first = lnode & ((1u << 27) - 1u);
+        uint32_t count = (node >> 27) & 0xFu;
+        const uint32_t first = node & ((1u << 27) - 1u);
 #ifdef YART_WALK_CHECK
         if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
 #endif
@@ -1254,12 +1217,6 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
             }
           }
         }
-#if YART_COOP_SPEC
-        if (pl != 0u) {  // the parked leaf was tested: a leaf at `node` takes its place, else `node` stays
-          pl = (node >> 31) ? node : 0u;
-          popped = !(node >> 31);
-        }
-#endif
       } else {
 #ifdef YART_WALK_CHECK
         if (node >= M.n_nodes) { walk_fault(4u); node = root; }
@@ -1315,31 +1272,16 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
 #endif
           node = nx;
           popped = true;
-#if YART_COOP_SPEC
-          if (f2b && (nx >> 31) && pl == 0u) { pl = nx; popped = false; }  // park it, take the next entry
-#endif
         }
       }
       if (!popped) {
         for (;;) {  // front to back: entries whose box begins beyond the bound are dropped
-#if YART_COOP_SPEC
-          if (cursor == 0) { node = kCoopSent; break; }
-          cursor -= 1;
-          node = qstk[cursor * 16 + (int)q];
-          if (f2b && __uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound) continue;
-          if (f2b && (node >> 31) && pl == 0u) { pl = node; continue; }  // park the first leaf
-          break;
-#else
           if (cursor == 0) { fin = true; break; }
           cursor -= 1;
           node = qstk[cursor * 16 + (int)q];
           if (!f2b || !(__uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound)) break;
-#endif
         }
       }
-#if YART_COOP_SPEC
-      fin = node == kCoopSent && pl == 0u;
-#endif
       if (kPostCheck && fin && c == 0)  // the ray's own lane checks W after the walk (below)
         rays[ray].flags = (f2b && fnd) ? (0x80000000u | bleaf) : 0u;
       if (!kPostCheck && fin && f2b && fnd) {
@@ -1523,7 +1465,7 @@ __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
 template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                              LightCap* cap = nullptr, bool prio = false) {
+                                              LightCap* cap = nullptr) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -1536,7 +1478,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st, prio);
+      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1737,12 +1679,12 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
 template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
                                           int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                          LightCap* cap = nullptr, bool prio = false) {
+                                          LightCap* cap = nullptr) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap, prio) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -2361,7 +2303,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
     if (__ballot(run) == 0) break;
     double R = 0.0;
-    bool term = false, want = false, sec = false;  // sec: this iteration scattered (not a camera ray)
+    bool term = false, want = false;
     // LPF: a Lambertian scatter's mixture pdf waits for the world pass of the ray it sampled,
     // which captures the light hits pdf_value would re-test (device_types.h kMaxLpf): T·att·spdf
     // (Tp) and the cosine half (cosv) are kept until then, T stays the incoming throughput.
@@ -2444,7 +2386,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         fresh = false;
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
         PROF(PF_SCATTER);
-        sec = true;
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
         auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
@@ -2500,13 +2441,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         PROF(PF_WORLD);
         DUP_LOOP(3) {
         DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
-        bool prio = false;  // YART_COOP_PRIO: rays expected to walk long go first in the mesh walk's pool
-#if YART_COOP_PRIO == 1
-        prio = sec && S.materials[hmat].kind == YART_MAT_DIELECTRIC;  // inside or into glass
-#elif YART_COOP_PRIO == 2
-        prio = sec;  // every secondary ray
-#endif
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q, nullptr, prio);
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
         DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
         }
       } else if (want) {
