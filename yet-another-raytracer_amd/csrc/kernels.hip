@@ -1084,21 +1084,16 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
   const __attribute__((address_space(1))) LeafAux* aux = (const __attribute__((address_space(1))) LeafAux*)M.aux;
   const uint32_t root = M.root, wroot = M.wroot;  // reference tree / walk tree (front to back)
-  const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
-  // Each lane forms its own ray's record before the pool is laid out (coop_stage).
+  // The cull test first (its constants discarded), then the record formed and written in one
+  // block, as before the cull: held across the pool's ballot, the constants cost the walk loop
+  // registers.
   bool walk = false;
-  CoopStage g0{};
-  if (want) {
-    g0 = coop_stage(M, aux != nullptr, r, tmin32, tmax_in);
-    walk = g0.walk;
-  }
-  uint64_t act = __ballot(walk);
+  if (want) walk = coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in).walk;
+  const uint64_t act = __ballot(walk);
+  if (act == 0) return;
   const uint32_t n = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  if (walk) {
-    coop_write(rays[rank], r, tmax_in, g0);
-  }
-  if (n == 0) return;
+  if (walk) coop_write(rays[rank], r, tmax_in, coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in));
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
@@ -1108,6 +1103,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
   double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
+  const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
   float inv32[3], teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
   vfloat2 c32[3];
   float bound = INFINITY;  // front to back: a popped entry beyond this is dropped
@@ -1319,8 +1315,6 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   // lane checks its own ray once, after the walk, instead of the whole wave at every ray's end. A
   // ray that fails walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in this
   // wave's LDS, free once every lane has read its record) — rare.
-  uint32_t* const lane_stk = reinterpret_cast<uint32_t*>(lds) + lane;
-  const bool force = __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
   bool redo = false;
   if (walk) {
     const CoopRay& s = rays[rank];
@@ -1329,13 +1323,14 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
     t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
     tri = (uint32_t)res;
     const uint32_t fl = s.flags;
-    if (kPostCheck && (fl >> 31)) redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || force;
+    if (kPostCheck && (fl >> 31))
+      redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
   }
   if (kPostCheck && __ballot(redo) != 0ull) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (redo) {
       if (STATS) st.v[ST_REWALK]++;
-      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, lane_stk, st);
+      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
     }
   }
 }
