@@ -261,6 +261,36 @@ def test_box_cull_is_exact_on_grazing_rays(dev):
     _hits_equal(h, o, h2, o2)
 
 
+@pytest.mark.parametrize("scene", ["sycee", "david"])
+def test_mesh_cull_box_is_exact_on_grazing_rays(dev, scene):
+    """A ray whose conservative f32 test misses a mesh's cull box (the union of both roots' child
+    boxes, DevMesh::box_lo/hi) is left out of the cooperative walk. Rays aimed at the box's faces,
+    edges and corners — nudged by 1e-16..1e-7 relative either way, from outside and inside, with
+    infinite and finite t_max — must hit exactly as the oracle's walk of the reference tree."""
+    p = yart.Preset(scene)
+    m = p.desc.contents.meshes[0]
+    pos = np.ctypeslib.as_array(m.positions, shape=(m.n_triangles * 9,)).reshape(-1, 3).astype(np.float64)
+    lo, hi = pos.min(0), pos.max(0)  # the first list entry holds the mesh without a wrapper
+    rng = np.random.default_rng(51)
+    n = 150000
+    tgt = rng.uniform(lo, hi, (n, 3))
+    ax = rng.integers(0, 3, n)
+    tgt[np.arange(n), ax] = np.where(rng.random(n) < 0.5, lo[ax], hi[ax])  # on a face
+    pin = rng.random(n) < 0.4  # on an edge or (with a third pin) a corner
+    ax2 = (ax + 1 + rng.integers(0, 2, n)) % 3
+    tgt[pin, ax2[pin]] = np.where(rng.random(pin.sum()) < 0.5, lo[ax2[pin]], hi[ax2[pin]])
+    tgt = tgt * (1.0 + rng.choice([-1.0, 0.0, 1.0], (n, 3)) * 10.0 ** rng.uniform(-16, -7, (n, 3)))
+    span = hi - lo
+    org = lo - span + rng.random((n, 3)) * 3.0 * span
+    dirs = tgt - org
+    rays = np.concatenate([org, dirs, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+    rays[::5, 7] = rng.uniform(0.9, 1.1, len(rays[::5]))  # t_max around the box face (|dirs| reaches it at t = 1)
+    h, o = yart.DeviceScene(p.desc).intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o2 >= 0).mean() > 0.02 and (o2 < 0).mean() > 0.05
+    _hits_equal(h, o, h2, o2)
+
+
 @pytest.mark.parametrize("scene", ["cornell-box", "three-spheres", "two-spheres", "random-scene"])
 def test_world_bvh_forced_on_matches_linear_scan(dev, scene, monkeypatch):
     """YART_WORLD_BVH=1 puts every boxable list behind the world BVH (wrappers, boxes, flipped
