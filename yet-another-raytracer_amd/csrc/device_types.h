@@ -115,9 +115,13 @@ struct alignas(16) DevWorldNode {
   float bmax[3];
   uint32_t count;   // 0 = inner node
   uint32_t first;   // inner: left child (right = first + 1); leaf: first slot in world_objs
-  uint32_t pad[3];  // pad[0]: leaf flags (kWorldLeafSpheres)
+  uint32_t pad[3];  // pad[0]: leaf flags (kWorldLeafSpheres); pad[1]: the node's handle (below)
 };
 constexpr uint32_t kWorldLeafSpheres = 1u;  // every object of the leaf is a sphere without wrappers
+// A node's handle: count << 28 | (kWorldLeafSpheres ? 1 << 27) | first — everything the walk needs
+// to take the node, so descending and popping cost no dependent read of the node's own record.
+constexpr uint32_t kWorldHandleMaxCount = 15u;
+constexpr uint32_t kWorldHandleFirstMask = 1u << 27;
 static_assert(sizeof(DevWorldNode) == 48, "DevWorldNode must be 48 B");
 
 struct DevScene {

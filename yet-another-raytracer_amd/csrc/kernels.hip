@@ -1594,13 +1594,14 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
-  uint32_t node = 0;
+  // the walk carries node handles (DevWorldNode::pad[1]), read with the child boxes: descending
+  // and popping take a node without a dependent read of its own record
+  uint32_t hnd = S.world_nodes[0].pad[1];
   int cursor = 0;
   for (;;) {
-    const DevWorldNode& N = S.world_nodes[node];
-    const uint32_t count = N.count, first = N.first;
+    const uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
     bool pop = true;
-    if (count && YART_WORLD_SPH && (N.pad[0] & kWorldLeafSpheres)) {
+    if (count && YART_WORLD_SPH && ((hnd >> 27) & 1u)) {
       // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
       // object records and the kind switch; the same sphere_t on the same values
       for (uint32_t k = 0; k < count; ++k) {
@@ -1633,9 +1634,11 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       thi = thi + fabsf(thi) * 0x1p-10f;
       float entry[2];
       bool hit[2];
+      uint32_t ch[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const DevWorldNode& C = S.world_nodes[first + c];
+        ch[c] = C.pad[1];
         const float m = (C.mag + O) * 0x1p-12f;
         float lo = tlo, hi = thi;
 #pragma unroll
@@ -1651,20 +1654,20 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       }
       if (STATS) st.v[ST_NODES]++;
       if (hit[0] && hit[1]) {
-        const uint32_t near = entry[0] <= entry[1] ? first : first + 1;
-        stk[cursor * 64] = near == first ? first + 1 : first;
+        const bool n0 = entry[0] <= entry[1];
+        stk[cursor * 64] = n0 ? ch[1] : ch[0];
         cursor++;
-        node = near;
+        hnd = n0 ? ch[0] : ch[1];
         pop = false;
       } else if (hit[0] || hit[1]) {
-        node = hit[0] ? first : first + 1;
+        hnd = hit[0] ? ch[0] : ch[1];
         pop = false;
       }
     }
     if (pop) {
       if (cursor == 0) break;
       cursor--;
-      node = stk[cursor * 64];
+      hnd = stk[cursor * 64];
     }
   }
   id.t = closest;

@@ -222,6 +222,12 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     }
     n.pad[0] = all ? kWorldLeafSpheres : 0u;
   }
+  // Each node's handle (pad[1]): what the walk needs to take the node without reading its record
+  // (the parent's child-box test reads the handle with the box, and the stack holds handles).
+  for (DevWorldNode& n : out.nodes) {
+    if (n.count > kWorldHandleMaxCount || n.first >= kWorldHandleFirstMask) return false;  // the list walk then
+    n.pad[1] = (n.count << 28) | ((n.pad[0] & kWorldLeafSpheres) ? (1u << 27) : 0u) | n.first;
+  }
   return out.depth < (uint32_t)kStackSlots;
 }
 
