@@ -256,7 +256,12 @@ int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lo
 /* Render into a DEVICE buffer on a caller stream (hipStream_t, NULL = default stream).
  * d_xyz_sum: width*height*3 doubles on the scene's device, per-pixel sums of the sanitised
  * sample XYZ (main.rs:690-708). Only this shard's blocks are written; the caller zeroes the
- * buffer if it wants the rest to read 0. Asynchronous: returns after the launch. */
+ * buffer if it wants the rest to read 0. Asynchronous: returns after the launch — except on the
+ * wavefront path (meshes deeper than depth 10, or YART_OPT_MESH_WAVEFRONT = 1), whose number of
+ * iterations is data-dependent: there the calling thread stays in the launch loop until the frame's
+ * last iteration is queued (the device may still be finishing it on return), and progress words
+ * move only at the end of the frame. The same holds for yart_render_packed_async and
+ * yart_render_multi_async on such scenes. */
 int yart_render_async(yart_scene* scene, const yart_camera* cam, const yart_render_params* p,
                       double* d_xyz_sum, void* hip_stream);
 
@@ -329,6 +334,10 @@ int yart_gather_frame_async(yart_comm* comm, const double* d_packed, uint32_t wi
  * work already queued on `hip_stream` (a stream of devices[0]), which then waits for the frame.
  * Frames submitted on different caller streams overlap on the devices; their gathers run in
  * submission order on every device. Bitwise yart_render on one device: each pixel has one writer.
+ * Each caller stream gets its own set of device streams and buffers, made on its first frame and
+ * kept for the next; at most 8 such sets live at once, and a ninth caller stream takes over the
+ * least recently used set after that set's frames have finished. All are freed by
+ * yart_multi_destroy.
  *
  * yart_render_multi is the same submission with host output and an optional progress callback
  * (pixels over all devices, on the calling thread); it waits for the frame and copies it to
@@ -405,6 +414,26 @@ int yart_probe_math(int device, int op, const double* a, const double* b, uint32
  * order (the per-lane walk the exact post-walk check falls back to), for the frames rendered on
  * this device until it is called with on = 0. The result is the same; only slower. */
 int yart_debug_force_rewalk(int device, int on);
+
+/* Test and tuning hooks, process-wide. The library reads no environment variable: every switch
+ * that changes how it builds or renders (never what it computes — each setting gives the same
+ * bits) is one of these, read at the next yart_scene_create (build and path choices) or frame
+ * (scratch budget). The defaults are the shipped behaviour; tests set them and restore them. */
+enum {
+  YART_OPT_QBVH_TIES_DESC = 0, /* 0 | 1: equal centroid keys in descending input order (the probe of
+                                  sort_unstable_by's freedom, qbvh.rs:679-685)                      */
+  YART_OPT_QBVH_THREADS = 1,   /* host builder threads, 0 = the hardware's concurrency              */
+  YART_OPT_WALK_TREE = 2,      /* 1 | 0: build the SAH walk tree / walk the reference tree front to back */
+  YART_OPT_MESH_WALK_REF = 3,  /* 0 | 1: every mesh ray walks in the reference's order (qbvh.rs:381-543) */
+  YART_OPT_WORLD_BVH = 4,      /* -1 auto (>= 16 objects, no mesh) | 0 never | 1 whenever every object has a box */
+  YART_OPT_MESH_WAVEFRONT = 5, /* -1 auto (meshes deeper than depth 10) | 0 never (those are refused) |
+                                  1 every mesh scene without media / moving spheres / noise or image textures */
+  YART_OPT_WF_POOL = 6,        /* wavefront path slots, >= 256 (rounded down to a multiple of 256), default 2^20 */
+  YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass in bytes, default 4 GiB        */
+  YART_OPT_COUNT = 8
+};
+int yart_debug_set_option(int option, int64_t value);
+int yart_debug_get_option(int option, int64_t* value);
 
 #ifdef __cplusplus
 }

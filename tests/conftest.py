@@ -15,3 +15,19 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def repo():
     return REPO
+
+
+@pytest.fixture
+def opt():
+    """opt("world_bvh", 1): sets a library option (yart_debug_set_option, include/yart.h YART_OPT_*)
+    for this test and restores every option it touched afterwards."""
+    import yart
+    saved = {}
+
+    def set_(name, value):
+        old = yart.set_option(name, value)
+        saved.setdefault(name, old)
+
+    yield set_
+    for k, v in saved.items():
+        yart.set_option(k, v)

@@ -165,6 +165,33 @@ def test_render_multi_async_on_one_device_is_the_render():
     m.close()
 
 
+def test_wavefront_frames_back_to_back_on_one_stream():
+    """ADVICE r03 (status-ring race): on the wavefront path a pass ends at a data-dependent
+    iteration j while iterations j+1 .. j+6 are still queued; the next pass or frame on the same
+    stream must not re-arm a status slot one of them has yet to write. Twelve frames of different
+    spp (so the pass lengths, and the j at which each ends, differ), some split into one-sample
+    scratch passes, enqueued back to back on ONE stream with no host wait between them and a small
+    path pool (hundreds of iterations per pass): each must be bitwise its megakernel render."""
+    p = yart.Preset("bunny")
+    W, H = 24, 24
+    cam = p.camera(W, H)
+    spps = [1, 2, 3, 5, 4, 7, 6, 8, 2, 9, 3, 5]
+    with yart.option("mesh_wavefront", 0):
+        mega = yart.DeviceScene(p)
+        refs = [mega.render(cam, yart.render_params(W, H, spp, 50)) for spp in spps]
+    with yart.option("mesh_wavefront", 1), yart.option("wf_pool", 256):
+        wf = yart.DeviceScene(p)
+    st = torch.cuda.current_stream()
+    outs = [torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0") for _ in spps]
+    for k, (spp, out) in enumerate(zip(spps, outs)):
+        budget = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 24 * (1 if k % 3 == 1 else 64)  # every third: one sample per pass
+        with yart.option("scratch_bytes", budget):
+            wf.render_async(cam, yart.render_params(W, H, spp, 50), out.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    for k, (out, ref) in enumerate(zip(outs, refs)):
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"frame {k} (spp {spps[k]})")
+
+
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_unpack_of_n_packed_shards_is_the_render(n):
     """The root side of the N-rank gather without the transport: shard k rendered by

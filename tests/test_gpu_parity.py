@@ -174,7 +174,7 @@ def test_intersect_matches_oracle(dev, scene):
 
 
 @pytest.mark.parametrize("scene,render", [("david", ("david", 48, 27, 2)), ("sycee", ("bunny", 40, 40, 4))])
-def test_qbvh_tie_order_does_not_change_hits(dev, scene, render, monkeypatch):
+def test_qbvh_tie_order_does_not_change_hits(dev, scene, render, opt):
     """The reference sorts split ranges with sort_unstable_by (qbvh.rs:679-685), so the order of
     equal centroid keys — and with it leaf membership and lane order at 3,943 of david's cuts — is
     not pinned. Build the BLAS a second time with the opposite tie order and require the same
@@ -192,7 +192,7 @@ def test_qbvh_tie_order_does_not_change_hits(dev, scene, render, monkeypatch):
     rp = yart.Preset(render[0])
     cam, prm = rp.camera(render[1], render[2]), yart.render_params(render[1], render[2], render[3], 50)
     ra = yart.DeviceScene(rp.desc).render(cam, prm)
-    monkeypatch.setenv("YART_QBVH_TIES", "desc")
+    opt("qbvh_ties_desc", 1)
     b = yart.DeviceScene(p.desc)
     assert b.info().bvh_tied_cuts > 0 and a.info().bvh_tied_cuts > 0
     hb, ob = b.intersect(rays)
@@ -292,10 +292,10 @@ def test_mesh_cull_box_is_exact_on_grazing_rays(dev, scene):
 
 
 @pytest.mark.parametrize("scene", ["cornell-box", "three-spheres", "two-spheres", "random-scene"])
-def test_world_bvh_forced_on_matches_linear_scan(dev, scene, monkeypatch):
-    """YART_WORLD_BVH=1 puts every boxable list behind the world BVH (wrappers, boxes, flipped
+def test_world_bvh_forced_on_matches_linear_scan(dev, scene, opt):
+    """The world_bvh option = 1 puts every boxable list behind the world BVH (wrappers, boxes, flipped
     light included): closest hits and renders stay bitwise the oracle's linear HittableList."""
-    monkeypatch.setenv("YART_WORLD_BVH", "1")
+    opt("world_bvh", 1)
     p = yart.Preset(scene)
     s = yart.DeviceScene(p)
     assert s.info().world_nodes > 0
@@ -328,13 +328,10 @@ def test_world_bvh_ties_go_to_the_later_object(dev):
     d = b.desc()
     rays = _random_rays(60000, -9, 9, seed=17)
     h2, o2 = O.OracleScene(d).intersect(rays)
-    for force in ("1", "0"):
-        os_env = {"YART_WORLD_BVH": force}
-        with pytest.MonkeyPatch.context() as mp:
-            for k, v in os_env.items():
-                mp.setenv(k, v)
+    for force in (1, 0):
+        with yart.option("world_bvh", force):
             s = yart.DeviceScene(d)
-            assert (s.info().world_nodes > 0) == (force == "1")
+            assert (s.info().world_nodes > 0) == (force == 1)
             h, o = s.intersect(rays)
         assert (o2 >= 0).mean() > 0.15
         _hits_equal(h, o, h2, o2)
@@ -363,8 +360,7 @@ def test_world_bvh_sphere_leaves_beside_wrapped_and_hollow_spheres(dev):
     d = b.desc()
     rays = _random_rays(60000, -8, 8, seed=29)
     h2, o2 = O.OracleScene(d).intersect(rays)
-    with pytest.MonkeyPatch.context() as mp:
-        mp.setenv("YART_WORLD_BVH", "1")
+    with yart.option("world_bvh", 1):
         s = yart.DeviceScene(d)
         assert s.info().world_nodes > 0
         h, o = s.intersect(rays)
@@ -462,14 +458,14 @@ def test_chunked_samples_bitwise_equal_to_sequential_sum(dev, scene, spu):
     np.testing.assert_array_equal(chunked, O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
 
 
-def test_chunked_multi_pass_and_shards(dev, monkeypatch):
+def test_chunked_multi_pass_and_shards(dev, opt):
     """A scratch budget of a few samples forces several accumulate passes; with shards too."""
     p = yart.Preset("cornell-box")
     W, H, spp = 48, 40, 10
     cam = p.camera(W, H)
     s = yart.DeviceScene(p)
     ref = O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50))
-    monkeypatch.setenv("YART_SCRATCH_BYTES", str(3 * 48 * 64 * 24))  # 3 samples x (48/8*40/8 blocks)
+    opt("scratch_bytes", 3 * 48 * 64 * 24)  # 3 samples x (48/8*40/8 blocks)
     parts = [s.render(cam, yart.render_params(W, H, spp, 50, shard_index=i, shard_count=2, samples_per_unit=1))
              for i in range(2)]
     np.testing.assert_array_equal(parts[0] + parts[1], ref)
@@ -498,21 +494,21 @@ def test_shards_partition_the_frame(dev):
 
 @pytest.mark.parametrize("scene,W,H,spp,depth", [("bunny", 40, 40, 4, 50), ("david", 48, 27, 2, 50), ("david", 24, 16, 3, 1),
                                                  ("david", 16, 16, 2, 0)])
-def test_wavefront_and_megakernel_agree(dev, scene, W, H, spp, depth, monkeypatch):
-    """The wavefront path (k_wf_shade / k_wf_trace; YART_MESH_WF=1, the default only for meshes
-    deeper than depth 10) must give the megakernel's bits (YART_MESH_WF=0) and the oracle's: with
+def test_wavefront_and_megakernel_agree(dev, scene, W, H, spp, depth, opt):
+    """The wavefront path (k_wf_shade / k_wf_trace; option mesh_wavefront = 1, the default only for
+    meshes deeper than depth 10) must give the megakernel's bits (mesh_wavefront = 0) and the oracle's: with
     the default pool, with a 256-path pool (hundreds of iterations, every path slot regenerated
     many times), and over several scratch passes."""
     p = yart.Preset(scene)
     cam = p.camera(W, H)
     prm = yart.render_params(W, H, spp, depth)
-    monkeypatch.setenv("YART_MESH_WF", "1")
+    opt("mesh_wavefront", 1)
     wf = yart.DeviceScene(p).render(cam, prm)
-    monkeypatch.setenv("YART_WF_POOL", "256")
+    opt("wf_pool", 256)
     small = yart.DeviceScene(p).render(cam, prm)
-    monkeypatch.setenv("YART_SCRATCH_BYTES", str(((W + 7) // 8) * ((H + 7) // 8) * 64 * 24))  # one sample per pass
+    opt("scratch_bytes", ((W + 7) // 8) * ((H + 7) // 8) * 64 * 24)  # one sample per pass
     passes = yart.DeviceScene(p).render(cam, prm)
-    monkeypatch.setenv("YART_MESH_WF", "0")
+    opt("mesh_wavefront", 0)
     mega = yart.DeviceScene(p).render(cam, prm)
     np.testing.assert_array_equal(wf, mega)
     np.testing.assert_array_equal(small, mega)
@@ -574,14 +570,10 @@ def test_deep_mesh_walks_with_the_references_64_slot_stack(dev):
     img = s.render(cam, prm)
     np.testing.assert_array_equal(img, o.render(cam, prm, threads=0))
     assert (img[O.coverage(24, 24)].sum(axis=-1) != 0).mean() > 0.5
-    import os
-    os.environ["YART_MESH_WF"] = "0"
-    try:
+    with yart.option("mesh_wavefront", 0):
         with pytest.raises(yart.YartError) as e:
             yart.DeviceScene(desc)
         assert e.value.code == abi.ERR_UNSUPPORTED
-    finally:
-        del os.environ["YART_MESH_WF"]
 
 
 def test_finalize_matches_oracle(dev):

@@ -20,7 +20,7 @@ for s in $STEPS; do
     rehearse) YART_BENCH_SAME_DEVICE=1 run rehearse 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 2 --warmup 1 --no-stats --cpu-spp 0 ;;
     configs) run configs 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
-    configs_ref) YART_MESH_WALK=ref run configs_ref 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
-    configs_mega) YART_MESH_WF=0 run configs_mega 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
+    configs_ref) YART_OPTIONS=mesh_walk_ref=1 run configs_ref 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
+    configs_mega) YART_OPTIONS=mesh_wavefront=0 run configs_mega 600 python tools/bench_configs.py --spp-scale ${SPP_SCALE:-0.125} ${CONFIG_ARGS:-} ;;
   esac
 done

@@ -20,7 +20,7 @@ for s in $STEPS; do
     pytest) run mesh_pytest 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 150 --timeout-method thread \
               -k "${PYTEST_K:-david or sycee or bunny or qbvh or C4 or C5}" ;;
     configs) run mesh_configs 600 python tools/bench_configs.py --configs ${CONFIGS:-C4,C5} --spp-scale ${SPP_SCALE:-0.0625} ;;
-    configs_ref) YART_MESH_WALK=ref run mesh_configs_ref 600 python tools/bench_configs.py --configs ${CONFIGS:-C4,C5} --spp-scale ${SPP_SCALE:-0.0625} ;;
+    configs_ref) YART_OPTIONS=mesh_walk_ref=1 run mesh_configs_ref 600 python tools/bench_configs.py --configs ${CONFIGS:-C4,C5} --spp-scale ${SPP_SCALE:-0.0625} ;;
     ab) run mesh_ab 900 python tools/ab.py yet-another-raytracer_amd/lib/libyart.so ${AB_LIBS:-} --scene ${AB_SCENE:-david} \
           --w ${AB_W:-1920} --h ${AB_H:-1080} --spp ${AB_SPP:-16} --reps 2 ;;
   esac

@@ -21,7 +21,7 @@ for s in $STEPS; do
       for sc in "bunny 800 800 32" "david 1920 1080 16"; do
         set -- $sc
         run ab_walk_$1 600 python3 tools/ab.py $L/libyart.so --scene $1 --w $2 --h $3 --spp $4 --reps 3
-        YART_WALK_TREE=0 run ab_refwalk_$1 600 python3 tools/ab.py $L/libyart.so --scene $1 --w $2 --h $3 --spp $4 --reps 3
+        YART_OPTIONS=walk_tree=0 run ab_refwalk_$1 600 python3 tools/ab.py $L/libyart.so --scene $1 --w $2 --h $3 --spp $4 --reps 3
       done ;;
   esac
 done

@@ -16,6 +16,5 @@ run() {
 run world_pytest 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread \
   -k "${PYTEST_K:-world_bvh or random or C3 or three-spheres}"
 run world_c3_sah 300 python tools/bench_configs.py --configs C3 --spp-scale ${SPP_SCALE:-0.0625}
-YART_WORLD_BVH_SPLIT=median run world_c3_median 300 python tools/bench_configs.py --configs C3 --spp-scale ${SPP_SCALE:-0.0625}
 run world_ab 600 python tools/ab.py yet-another-raytracer_amd/lib/libyart.so ${AB_LIBS:-} --scene random-scene --w 1200 --h 800 --spp 16 --reps 2
 echo ALL_OK

@@ -22,7 +22,7 @@ L.yart_debug_walk_fault.argtypes = [C.c_int, C.POINTER(C.c_uint)]
 bad = 0
 for scene, w, h, spp in [("bunny", 800, 800, 4), ("david", 1920, 1080, 2), ("david", 480, 270, 16)]:
     for walk_tree in ("1", "0"):
-        os.environ["YART_WALK_TREE"] = walk_tree
+        yart.set_option("walk_tree", int(walk_tree))
         p = yart.Preset(scene)
         s = yart.DeviceScene(p)
         img = s.render(p.camera(w, h), yart.render_params(w, h, spp, 50))

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <exception>
 #include <map>
 #include <thread>
 #include <cmath>
@@ -21,21 +22,33 @@ struct Box {
 };
 
 // Runs tasks[0] on this thread and the others on threads of their own where the system gives one;
-// a task whose thread cannot be created (std::system_error) runs here instead, so no exception
-// leaves the C ABI and the result is the same either way.
+// a task whose thread cannot be created (std::system_error) runs here instead, so the result is the
+// same either way. An exception inside a task (bad_alloc in a worker) is caught in that task, and
+// the first one is rethrown here after every thread has joined — to build_qbvh's handler, so it
+// becomes an error code at the C ABI instead of std::terminate.
 void run_all(std::vector<std::function<void()>>& tasks) {
+  std::vector<std::exception_ptr> err(tasks.size());
+  auto guarded = [&tasks, &err](size_t i) {
+    try {
+      tasks[i]();
+    } catch (...) {
+      err[i] = std::current_exception();
+    }
+  };
   std::vector<std::thread> th;
   std::vector<size_t> inline_tasks;
   for (size_t i = 1; i < tasks.size(); ++i) {
     try {
-      th.emplace_back(tasks[i]);
+      th.emplace_back(guarded, i);
     } catch (const std::system_error&) {
       inline_tasks.push_back(i);
     }
   }
-  if (!tasks.empty()) tasks[0]();
-  for (size_t i : inline_tasks) tasks[i]();
+  if (!tasks.empty()) guarded(0);
+  for (size_t i : inline_tasks) guarded(i);
   for (auto& t : th) t.join();
+  for (const auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 // ORDER_TABLE (qbvh.rs:14-16) row for a node's split axes (top | left << 2 | right << 4) and a

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -28,6 +29,20 @@ namespace yart_impl {
 thread_local std::string g_err;
 int fail(int code, const std::string& m) { g_err = m; return code; }
 int ok() { g_err.clear(); return YART_OK; }
+
+// Test and tuning hooks (yart_debug_set_option): process-wide, read where the behaviour is decided
+// (scene creation, frame planning). The library reads no environment variable.
+static std::atomic<int64_t> g_opt[YART_OPT_COUNT] = {
+    {0},        // YART_OPT_QBVH_TIES_DESC
+    {0},        // YART_OPT_QBVH_THREADS (0 = hardware concurrency)
+    {1},        // YART_OPT_WALK_TREE
+    {0},        // YART_OPT_MESH_WALK_REF
+    {-1},       // YART_OPT_WORLD_BVH
+    {-1},       // YART_OPT_MESH_WAVEFRONT
+    {1 << 20},  // YART_OPT_WF_POOL
+    {4ll << 30} // YART_OPT_SCRATCH_BYTES
+};
+int64_t opt(int k) { return k >= 0 && k < YART_OPT_COUNT ? g_opt[k].load(std::memory_order_relaxed) : 0; }
 int hip_fail(hipError_t e, const char* what) {
   return fail(YART_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -111,39 +126,7 @@ DevObject to_dev(const yart_object& o) {
     }
   }
   for (int k = 0; k < 24; ++k) d.p[k] = o.p[k];
-  d.lpf = kNoLpf;
   return d;
-}
-
-// Light-pdf capture slots (device_types.h): every light whose pdf_value intersects (no wrapper,
-// XZRect or StillSphere: hittable.rs:28-30 gives the others 0) is paired with a world object that
-// is the same primitive — same kind and parameters, no wrapper but FlipFace (which leaves the ray
-// and t alone) — so the world pass of the sampled ray yields exactly the t and hit pdf_value
-// computes. All or nothing: a light without a partner, or more than kMaxLpf of them, leaves the
-// scene on the reference's re-intersection. YART_LPF=0 forces that (A/B).
-uint32_t assign_lpf(std::vector<DevObject>& objs, std::vector<DevObject>& lights) {
-  if (const char* e = std::getenv("YART_LPF"))
-    if (std::atoi(e) == 0) return 0;
-  uint32_t n = 0;
-  for (DevObject& l : lights) {
-    if (l.n_xf != 0 || (l.kind != YART_PRIM_XZ_RECT && l.kind != YART_PRIM_SPHERE)) continue;
-    const int np = l.kind == YART_PRIM_SPHERE ? 4 : 5;
-    DevObject* partner = nullptr;
-    for (DevObject& o : objs) {
-      if (o.kind != l.kind || o.lpf != kNoLpf) continue;
-      bool same = true, plain = o.n_xf <= (uint32_t)kMaxXforms;
-      for (int k = 0; k < np; ++k) same &= std::memcmp(&o.p[k], &l.p[k], sizeof(double)) == 0;
-      for (uint32_t w = 0; w < o.n_xf && w < (uint32_t)kMaxXforms; ++w) plain &= o.xf_kind[w] == YART_XF_FLIP_FACE;
-      if (same && plain) { partner = &o; break; }
-    }
-    if (!partner || n == kMaxLpf) {
-      for (DevObject& o : objs) o.lpf = kNoLpf;
-      for (DevObject& x : lights) x.lpf = kNoLpf;
-      return 0;
-    }
-    partner->lpf = l.lpf = n++;
-  }
-  return n;
 }
 
 }  // namespace
@@ -183,7 +166,7 @@ int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lo
   return rc ? fail(rc, "null argument") : ok();
 }
 
-int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
+static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   if (!d || !out) return fail(YART_ERR_INVALID, "null argument");
   if (d->abi_version != YART_ABI_VERSION) return fail(YART_ERR_INVALID, "abi_version mismatch");
   if ((d->n_objects && !d->objects) || (d->n_lights && !d->lights) || (d->n_materials && !d->materials) ||
@@ -244,18 +227,17 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   std::vector<BuiltMesh> built(d->n_meshes);
   uint32_t nodes = 0, leaves = 0, depth = 0, tied_cuts = 0, tied_leaves = 0, walk_nodes = 0, walk_depth = 0;
   double build_ms = 0.0;
-  QbvhOptions qopt;  // YART_QBVH_TIES=desc: the tie-order probe (tests); YART_QBVH_THREADS=n
-  if (const char* e = std::getenv("YART_QBVH_TIES")) qopt.ties_desc = std::strcmp(e, "desc") == 0;
-  if (const char* e = std::getenv("YART_QBVH_THREADS")) qopt.threads = (uint32_t)std::max(0, std::atoi(e));
+  QbvhOptions qopt;  // the tie-order probe (tests) and the builder's thread count
+  qopt.ties_desc = opt(YART_OPT_QBVH_TIES_DESC) != 0;
+  qopt.threads = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(opt(YART_OPT_QBVH_THREADS), 1024));
   for (uint32_t m = 0; m < d->n_meshes; ++m) {
     const yart_mesh& ym = d->meshes[m];
     if (!ym.positions || !ym.normals) return fail(YART_ERR_INVALID, "mesh without positions/normals");
     std::string err;
     if (!build_qbvh(ym.n_triangles, ym.positions, ym.normals, built[m], err, qopt)) return fail(YART_ERR_UNSUPPORTED, err);
-    // the front-to-back walk's own tree (walk_tree.cpp); YART_WALK_TREE=0 walks the reference tree
-    // front to back instead. Depth bound: the stack the walk gets (32 slots, 64 for deep meshes).
-    const char* wt = std::getenv("YART_WALK_TREE");
-    if (!(wt && std::atoi(wt) == 0)) {
+    // the front-to-back walk's own tree (walk_tree.cpp); YART_OPT_WALK_TREE = 0 walks the reference
+    // tree front to back instead. Depth bound: the stack the walk gets (32 slots, 64 for deep meshes).
+    if (opt(YART_OPT_WALK_TREE) != 0) {
       const uint32_t slots = 3 * built[m].depth + 1 > (uint32_t)kStackSlots ? (uint32_t)kMaxStackSlots : (uint32_t)kStackSlots;
       build_walk_tree(built[m], (slots - 1) / 3);
     }
@@ -269,27 +251,16 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     depth = std::max(depth, built[m].depth);
   }
 
-  // World BVH (world_bvh.h): for long object lists without meshes; YART_WORLD_BVH=0 / 1 forces
-  // the linear walk / the BVH (when every object has a box).
+  // World BVH (world_bvh.h): for long object lists without meshes; YART_OPT_WORLD_BVH = 0 / 1
+  // forces the linear walk / the BVH (when every object has a box).
   BuiltWorld world;
   bool use_world = false;
   {
     bool any_mesh = false;
     for (uint32_t i = 0; i < d->n_objects; ++i) any_mesh |= d->objects[i].kind == YART_PRIM_MESH;
-    const char* env = std::getenv("YART_WORLD_BVH");
-    const int force = env ? std::atoi(env) : -1;
+    const int64_t force = opt(YART_OPT_WORLD_BVH);
     const bool want = force == 1 || (force != 0 && d->n_objects >= kWorldBvhMinObjects);
-    // YART_WORLD_BVH_SPLIT=median: the round-1 median-split tree (A/B); default SAH
-    const char* split = std::getenv("YART_WORLD_BVH_SPLIT");
-    const bool sah = !(split && std::strcmp(split, "median") == 0);
-    if (want && !any_mesh) use_world = build_world_bvh(objs, world, sah);
-  }
-
-  uint32_t n_lpf = 0;
-  {
-    bool any_mesh = false;
-    for (uint32_t i = 0; i < d->n_objects; ++i) any_mesh |= d->objects[i].kind == YART_PRIM_MESH;
-    if (!use_world && !any_mesh) n_lpf = assign_lpf(objs, lights);  // the list kernels capture
+    if (want && !any_mesh) use_world = build_world_bvh(objs, world);
   }
 
   auto s = std::make_unique<yart_scene>();
@@ -327,10 +298,9 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
     }
     if (exact32) HIP_TRY(upload(s->owned, n32.data(), n32.size(), &dm[m].normals32, bytes), "upload normals");
     else HIP_TRY(upload(s->owned, b.normals.data(), b.normals.size(), &dm[m].normals, bytes), "upload normals");
-    // YART_MESH_WALK=ref: walk every ray in the reference's order (A/B and tests); default:
+    // YART_OPT_MESH_WALK_REF: walk every ray in the reference's order (A/B and tests); default:
     // front to back with the exact fallback (kernels.hip qbvh_coop)
-    const char* walk = std::getenv("YART_MESH_WALK");
-    if (!(walk && std::strcmp(walk, "ref") == 0))
+    if (opt(YART_OPT_MESH_WALK_REF) == 0)
       HIP_TRY(upload(s->owned, b.aux.data(), b.aux.size(), &dm[m].aux, bytes), "upload leaf records");
     dm[m].root = b.ref_nodes - 1;
     dm[m].n_nodes = (uint32_t)b.nodes.size();
@@ -362,7 +332,6 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
-  ds.n_lpf = n_lpf;
   ds.has_mesh = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
   ds.has_ext = 0;
@@ -377,21 +346,18 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   // Mesh scenes: the megakernel by default (A/B r03: the wavefront path is 18 % slower on david and
   // 47 % on the bunny stand-in); the wavefront path (k_wf_shade / k_wf_trace) for
   // meshes deeper than depth 10, which need more than the megakernel's 32 stack slots — its trace
-  // kernel walks them with the reference's 64 (qbvh.rs:382-384). YART_MESH_WF=1 puts every mesh
+  // kernel walks them with the reference's 64 (qbvh.rs:382-384). YART_OPT_MESH_WAVEFRONT = 1 puts every mesh
   // scene without EXT features (media, moving spheres, noise / image textures) on the wavefront
-  // path, YART_MESH_WF=0 none (deep meshes are then refused).
+  // path, 0 none (deep meshes are then refused).
   {
-    const char* e = std::getenv("YART_MESH_WF");
-    const int force = e ? std::atoi(e) : -1;
+    const int64_t force = opt(YART_OPT_MESH_WAVEFRONT);
     ds.deep = d->n_meshes && 3 * depth + 1 > (uint32_t)kStackSlots;
     s->wavefront = ds.has_mesh && !ds.has_ext && (force == 1 || (force != 0 && ds.deep));
     if (ds.deep && !s->wavefront)
       return fail(YART_ERR_UNSUPPORTED, "a mesh deeper than depth 10 renders on the wavefront path only (no media, "
-                                        "moving spheres or noise / image textures in its scene, YART_MESH_WF not 0)");
-    if (const char* pe = std::getenv("YART_WF_POOL")) {
-      const long v = std::atol(pe);
-      if (v >= 256) s->wf_pool = (uint32_t)std::min<long>(v, 1l << 24) / 256u * 256u;
-    }
+                                        "moving spheres or noise / image textures in its scene, YART_OPT_MESH_WAVEFRONT not 0)");
+    const int64_t pool = opt(YART_OPT_WF_POOL);
+    if (pool >= 256) s->wf_pool = (uint32_t)(std::min<int64_t>(pool, 1ll << 24) / 256 * 256);
   }
 
   yart_scene_info& in = s->info;
@@ -409,6 +375,16 @@ int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
   in.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - up0).count();
   *out = s.release();
   return ok();
+}
+
+int yart_scene_create(int device, const yart_scene_desc* d, yart_scene** out) {
+  try {  // nothing unwinds across the C ABI (host allocations of the builders)
+    return scene_create(device, d, out);
+  } catch (const std::bad_alloc&) {
+    return fail(YART_ERR_NO_MEMORY, "host allocation failed while building the scene");
+  } catch (const std::exception& e) {
+    return fail(YART_ERR_DEVICE, std::string("scene creation failed: ") + e.what());
+  }
 }
 
 void yart_scene_destroy(yart_scene* s) { delete s; }
@@ -454,6 +430,19 @@ int yart_qbvh_build(const float* positions, const double* normals, uint32_t n, u
 int yart_scene_get_info(const yart_scene* s, yart_scene_info* out) {
   if (!s || !out) return fail(YART_ERR_INVALID, "null argument");
   *out = s->info;
+  return ok();
+}
+
+int yart_debug_set_option(int option, int64_t value) {
+  if (option < 0 || option >= YART_OPT_COUNT) return fail(YART_ERR_INVALID, "unknown option");
+  g_opt[option].store(value, std::memory_order_relaxed);
+  return ok();
+}
+
+int yart_debug_get_option(int option, int64_t* value) {
+  if (!value) return fail(YART_ERR_INVALID, "null argument");
+  if (option < 0 || option >= YART_OPT_COUNT) return fail(YART_ERR_INVALID, "unknown option");
+  *value = opt(option);
   return ok();
 }
 
@@ -524,8 +513,7 @@ Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
     chunk = (uint32_t)((spp + chunks - 1) / chunks);
   }
   const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
-  uint64_t budget = 4ull << 30;
-  if (const char* e = std::getenv("YART_SCRATCH_BYTES")) budget = std::strtoull(e, nullptr, 0);
+  const uint64_t budget = (uint64_t)std::max<int64_t>(opt(YART_OPT_SCRATCH_BYTES), 1);
   uint64_t pass = budget / per_sample;
   pass = pass / chunk * chunk;
   if (pass < chunk) pass = chunk;
@@ -651,45 +639,44 @@ int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t str
   HIP_TRY(hipMemsetAsync(q.range, 0, (size_t)pool / 256 * 8, stream), "empty the job ranges");
   HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), stream), "zero the pass counters");
   volatile uint32_t* hs = st->wf_status_host;
-  static const bool log = std::getenv("YART_WF_LOG") != nullptr;  // per-pass iteration log (tools)
-  const auto t0 = std::chrono::steady_clock::now();
-  uint64_t polls = 0;
   WfArgs w;
   w.q = q;
   w.jobs = cnt + 4;
   w.total_jobs = (uint32_t)total;
   w.pool = pool;
-  w.resident = (uint32_t)s->cu_count * 16u;  // 4 waves per SIMD
+  // Status slots are numbered by the stream's iteration count, which runs on across passes and
+  // frames: when a pass ends at iteration j, its iterations j+1 .. j+kWfLookahead are still queued
+  // and each writes its own slot, so the next pass (which starts at the following number) never
+  // re-arms a slot one of them has yet to write (with the count restarting at 0 per
+  // pass, a trailing write could overwrite the next pass's sentinel and end that pass early).
+  // kWfStatusRing > 2 * kWfLookahead + 1 keeps the two passes' live slots apart.
+  static_assert(kWfStatusRing > 2 * kWfLookahead + 1, "status ring too small for the look-ahead");
+  const uint64_t base = st->wf_iter;
   for (uint32_t k = 0;; ++k) {
     if (k > (1u << 22)) return fail(YART_ERR_DEVICE, "wavefront pass did not finish");
-    __atomic_store_n(&hs[k % kWfStatusRing], kWfSentinel, __ATOMIC_RELAXED);
+    const uint32_t slot = (uint32_t)((base + k) % kWfStatusRing);
+    __atomic_store_n(&hs[slot], kWfSentinel, __ATOMIC_RELAXED);
     w.alive = cnt + k % 4;
     w.alive_next = cnt + (k + 1) % 4;
-    w.status = st->wf_status_dev + k % kWfStatusRing;
+    w.status = st->wf_status_dev + slot;
     HIP_TRY(launch_wf_shade(s->dev, b, w, stream), "launch k_wf_shade");
     HIP_TRY(launch_wf_trace(s->dev, b, w, stream), "launch k_wf_trace");
+    st->wf_iter = base + k + 1;
     if (k < kWfLookahead) continue;
-    const uint32_t j = k - kWfLookahead;
+    const uint32_t jslot = (uint32_t)((base + k - kWfLookahead) % kWfStatusRing);
     uint32_t v;
     for (int spin = 0;; ++spin) {
-      v = __atomic_load_n(&hs[j % kWfStatusRing], __ATOMIC_ACQUIRE);
+      v = __atomic_load_n(&hs[jslot], __ATOMIC_ACQUIRE);
       if (v != kWfSentinel) break;
       const hipError_t e = hipStreamQuery(stream);
       if (e != hipErrorNotReady) {
-        v = __atomic_load_n(&hs[j % kWfStatusRing], __ATOMIC_ACQUIRE);
+        v = __atomic_load_n(&hs[jslot], __ATOMIC_ACQUIRE);
         if (v != kWfSentinel) break;
         return e != hipSuccess ? hip_fail(e, "wavefront iteration") : fail(YART_ERR_DEVICE, "wavefront iteration did not report");
       }
       if (spin > 8) std::this_thread::sleep_for(std::chrono::microseconds(20));
-      ++polls;
     }
-    if (v == 0) {
-      if (log)
-        std::fprintf(stderr, "wf pass: %u jobs, pool %u, %u iterations (%u with rays), %llu polls, %.3f ms host\n",
-                     w.total_jobs, pool, k + 1, j, (unsigned long long)polls,
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-      break;
-    }
+    if (v == 0) break;
   }
   return YART_OK;
 }

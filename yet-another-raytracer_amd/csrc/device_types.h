@@ -25,19 +25,11 @@ constexpr int kBins = 36;
 constexpr int kStackSlots = 32;     // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
 constexpr int kMaxStackSlots = 64;  // the reference's stack (qbvh.rs:382-384): depth <= 21 (wavefront path)
 
-// Light-pdf capture (analytic list kernels): a light whose pdf_value re-intersects the sampled
-// ray (aarect.rs:148-162, sphere.rs:95-110) and the world object that is the same primitive share
-// a slot < kMaxLpf; the world pass records that object's t and hit over [0.001, inf) for the ray
-// it is tracing anyway, and the mixture pdf is finished from them (kernels.hip, k_render).
-constexpr uint32_t kMaxLpf = 2;
-constexpr uint32_t kNoLpf = 0xFFFFFFFFu;
-
 struct DevObject {
   uint32_t kind, material, mesh, n_xf;
   uint32_t xf_kind[kMaxXforms];
   double xf[kMaxXforms][3];  // TRANSLATE: offset; ROTATE_Y: sin, cos (hittable.rs:173-176)
   double p[24];
-  uint32_t lpf, pad_;        // light-pdf capture slot, kNoLpf if none
 };
 
 struct DevMaterial {
@@ -139,7 +131,6 @@ struct DevScene {
   uint32_t has_ext;  // noise/image textures, isotropic materials, media or moving spheres (EXT kernels)
   uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
-  uint32_t n_lpf;    // light-pdf capture slots in use (0: light_pdf intersects, as the reference)
   uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
 };
 

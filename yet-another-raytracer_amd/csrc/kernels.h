@@ -64,7 +64,6 @@ struct WfArgs {
   uint32_t* jobs;        // job counter of the pass (device)
   uint32_t total_jobs;   // n_blocks * s_count * 64
   uint32_t pool;         // a multiple of 256
-  uint32_t resident;     // trace waves resident at once (persistent trace grid)
   uint32_t* status;      // host-mapped: k_wf_trace stores this iteration's flag (0 = pass done)
 };
 hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream);

@@ -137,18 +137,10 @@ __device__ __forceinline__ bool flagged(const Ieee&) { return false; }
 // measurement after the register-liveness work, the Fast policy in every kernel vs Ieee in every
 // kernel: cornell (list, no EXT) 4,814 vs 4,716 Msamples/s, random-scene (world BVH) 1,464 vs
 // 1,514, david (mesh) 243.4 vs 243.3. So Fast runs where it wins, the plain list kernel; the
-// others keep Ieee (the second copy of the block costs them registers). YART_FAST_MATH forces
-// Fast everywhere, YART_FAST_LIST=0 forces Ieee everywhere.
-#ifndef YART_FAST_LIST
-#define YART_FAST_LIST 1
-#endif
+// others keep Ieee (the second copy of the block costs them registers).
 template <bool HAS_MESH, bool BVH, bool EXT>
 struct MathPolicy {
-#ifdef YART_FAST_MATH
-  typedef Fast type;
-#else
-  typedef typename std::conditional<YART_FAST_LIST && !HAS_MESH && !BVH && !EXT, Fast, Ieee>::type type;
-#endif
+  typedef typename std::conditional<!HAS_MESH && !BVH && !EXT, Fast, Ieee>::type type;
 };
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
@@ -380,22 +372,12 @@ __device__ __forceinline__ void rng_init(Rng& r, uint64_t seed, uint32_t pixel, 
   r.k0 = (uint32_t)seed; r.k1 = (uint32_t)(seed >> 32);
   r.c0 = 0; r.c1 = sample; r.c2 = pixel; r.c3 = stream; r.have = 0;
 }
-#ifdef YART_ATTR
-__device__ __forceinline__ uint32_t opaque_zero() { uint32_t z; asm volatile("v_mov_b32 %0, 0" : "=v"(z)); return z; }
-#endif
 __device__ __forceinline__ void philox(const Rng& r, uint32_t blk, uint32_t& o0, uint32_t& o1, uint32_t& o2, uint32_t& o3) {
   uint32_t c0 = blk, c1 = r.c1, c2 = r.c2, c3 = r.c3, k0 = r.k0, k1 = r.k1;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-#ifdef YART_PHILOX_MAD
-    // one v_mad_u64_u32 per product instead of v_mul_hi_u32 + v_mul_lo_u32
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-#else
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-#endif
     c0 = hi1 ^ c1 ^ k0; c1 = lo1; c2 = hi0 ^ c3 ^ k1; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
@@ -405,16 +387,14 @@ __device__ __forceinline__ void philox(const Rng& r, uint32_t blk, uint32_t& o0,
 template <bool LAUNDER>
 __device__ __forceinline__ void rng_phase(Rng& r, uint32_t pixel, uint32_t sample, uint32_t phase) {
   r.c1 = sample; r.c2 = pixel; r.c3 = phase << 2;
-#ifndef YART_NO_LAUNDER
   if (LAUNDER) {  // the analytic linear-list kernel: +0.5 % there, -2 % on the world-BVH kernel
-  // The key is loop-invariant. Hoisted, its 20-word round schedule sat in SGPRs all kernel long and
-  // was spilled to VGPR lanes (one v_readlane, a VALU instruction, per round key per iteration).
-  // Made opaque here, the schedule is recomputed with scalar adds at each phase start.
-  r.k0 = __builtin_amdgcn_readfirstlane(r.k0);  // uniform (the seed); says so where control diverged
-  r.k1 = __builtin_amdgcn_readfirstlane(r.k1);
-  asm volatile("" : "+s"(r.k0), "+s"(r.k1));
+    // The key is loop-invariant. Hoisted, its 20-word round schedule sat in SGPRs all kernel long and
+    // was spilled to VGPR lanes (one v_readlane, a VALU instruction, per round key per iteration).
+    // Made opaque here, the schedule is recomputed with scalar adds at each phase start.
+    r.k0 = __builtin_amdgcn_readfirstlane(r.k0);  // uniform (the seed); says so where control diverged
+    r.k1 = __builtin_amdgcn_readfirstlane(r.k1);
+    asm volatile("" : "+s"(r.k0), "+s"(r.k1));
   }
-#endif
   philox(r, 0u, r.b0, r.b1, r.b2, r.b3);
   philox(r, 1u, r.b4, r.b5, r.b6, r.b7);
   r.c0 = 2; r.have = 4;
@@ -509,25 +489,6 @@ __device__ __forceinline__ bool sphere_t(const double* p, const Ray& r, double t
   }
   return true;
 }
-// sphere_t that also reports whether a root lies in [t_min, inf) (pdf_value's test, sphere.rs:96).
-// Both roots are computed; the finite-t_max answer follows sphere_t's own steps.
-__device__ __forceinline__ bool sphere_t_cap(const double* p, const Ray& r, double tmin, double tmax, double& t, bool& hit_inf) {
-  V3 center = mk(p[0], p[1], p[2]);
-  double radius = p[3];
-  V3 oc = sub(r.o, center);
-  double a = len2(r.d);
-  double half_b = dot(oc, r.d);
-  double c = len2(oc) - radius * radius;
-  double disc = half_b * half_b - a * c;
-  hit_inf = false;
-  if (disc < 0.0) return false;
-  double sq = sqrt(disc);
-  const double t1 = (0.0 - half_b - sq) / a, t2 = (0.0 - half_b + sq) / a;
-  hit_inf = !(t1 < tmin) || !(t2 < tmin);  // inf < t never holds
-  if (!(t1 < tmin || tmax < t1)) { t = t1; return true; }
-  if (!(t2 < tmin || tmax < t2)) { t = t2; return true; }
-  return false;
-}
 template <bool UV = false, class M = Ieee>
 __device__ __forceinline__ void sphere_rec(const double* p, const Ray& r, double t, Hit& h, M&& m = M()) {
   V3 center = mk(p[0], p[1], p[2]);
@@ -591,32 +552,8 @@ __device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r,
 }
 
 // aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
-#ifndef YART_RECT_CULL
-#define YART_RECT_CULL 0
-#endif
-// Conservative f32 pre-test of a rect (A/B flag YART_RECT_CULL): the plane parameter and the
-// in-plane point in f32 with the bounds grown by 2^-12 (|bounds| + |o|) and t's range by 2^-10, so
-// it passes whenever the f64 test can; when no active lane of the wave passes, the f64 divide
-// and the point are skipped for the whole wave.
-template <int A, int B, int CC>
-__device__ __forceinline__ bool rect_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
-  const double* o = &r.o.x;
-  const double* d = &r.d.x;
-  const float dA = (float)d[A];
-  if (!(fabsf(dA) >= 1.0e-20f && fabsf(dA) <= 1.0e20f)) return true;
-  const float oA = (float)o[A], oB = (float)o[B], oC = (float)o[CC];
-  const float t = ((float)p[4] - oA) * __builtin_amdgcn_rcpf(dA);
-  const float mg = (fmaxf(fmaxf(fabsf((float)p[0]), fabsf((float)p[1])), fmaxf(fabsf((float)p[2]), fabsf((float)p[3]))) +
-                    fmaxf(fmaxf(fabsf(oA), fabsf(oB)), fabsf(oC))) * 0x1p-12f;
-  const float lo = (float)tmin, hi = (float)tmax;
-  if (t < lo - fabsf(lo) * 0x1p-10f - 1e-30f || t > hi + fabsf(hi) * 0x1p-10f + 1e-30f) return false;
-  const float x = oB + t * (float)d[B], y = oC + t * (float)d[CC];
-  const float ex = fabsf(t * (float)d[B]) * 0x1p-12f, ey = fabsf(t * (float)d[CC]) * 0x1p-12f;
-  return !(x < (float)p[0] - mg - ex || x > (float)p[1] + mg + ex || y < (float)p[2] - mg - ey || y > (float)p[3] + mg + ey);
-}
 template <int A, int B, int CC>
 __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
-  if (YART_RECT_CULL && __ballot(rect_may_hit<A, B, CC>(p, r, tmin, tmax)) == 0ull) return false;
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
@@ -626,19 +563,6 @@ __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmi
   double y = o[CC] + t * d[CC];
   if (x < p[0] || x > p[1] || y < p[2] || y > p[3]) return false;
   return true;
-}
-// rect_t that also reports the test over [t_min, inf) — the one pdf_value makes (aarect.rs:149):
-// the same t, and the bounds checked whatever t_max says. Returns rect_t's answer.
-template <int A, int B, int CC>
-__device__ __forceinline__ bool rect_t_cap(const double* p, const Ray& r, double tmin, double tmax, double& t, bool& hit_inf) {
-  const double* o = &r.o.x;
-  const double* d = &r.d.x;
-  const double num = p[4] - o[A], den = d[A];
-  t = num / den;
-  const double x = o[B] + t * d[B];
-  const double y = o[CC] + t * d[CC];
-  hit_inf = !(t < tmin) && !(x < p[0] || x > p[1] || y < p[2] || y > p[3]);  // t > inf never holds
-  return hit_inf && !(t > tmax);
 }
 // Record of an axis-aligned rect with plane axis `a` (0 yz, 1 xz, 2 xy); a runtime axis lets the
 // rect and box-face records of a wave share one code path.
@@ -672,9 +596,6 @@ __device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, 
 // face tests may be skipped. f32 rounding (~1e-7 relative) stays far inside m; rays with
 // non-finite components, or a direction component too small for f32, are never culled.
 __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
-#ifdef YART_NO_BOX_CULL
-  return true;
-#else
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
@@ -697,7 +618,6 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
     hi = fminf(hi, fmaxf(t0, t1));
   }
   return lo <= hi;
-#endif
 }
 
 // BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
@@ -970,24 +890,9 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
   return (uint32_t)((k1 < key) | ((k1 == key) & ((c ^ 1u) < c))) + (uint32_t)((k2 < key) | ((k2 == key) & ((c ^ 2u) < c))) +
          (uint32_t)((k3 < key) | ((k3 == key) & ((c ^ 3u) < c)));
 }
-#ifndef YART_COOP_POSTCHECK
-#define YART_COOP_POSTCHECK 1
-#endif
-#ifndef YART_COOP_CULL
-#define YART_COOP_CULL 1  // rays missing the mesh's cull box stay out of the walk (qbvh_coop)
-#endif
 // Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
 // reference's order, so the rare path is exercised on whole frames.
 __device__ uint32_t g_force_rewalk;
-#ifndef YART_COOP_LEAF_MIN
-#define YART_COOP_LEAF_MIN 1  // quads waiting at a leaf before a round runs the leaf branch
-#endif
-
-#ifdef YART_COOP_NOINLINE
-#define YART_COOP_ATTR __noinline__
-#else
-#define YART_COOP_ATTR __forceinline__  // inlined: +4% david, +11% bunny over a call (caller spills)
-#endif
 enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // per wave: lane 0 counts
 #ifdef YART_WALK_CHECK
 // Bounds-checked build of the cooperative walk (tools: make variant DEFS=-DYART_WALK_CHECK): every
@@ -997,7 +902,7 @@ __device__ unsigned int g_walk_fault;
 __device__ __forceinline__ void walk_fault(unsigned int bit) { atomicOr(&g_walk_fault, bit); }
 #endif
 // A ray's walk record (CoopRay) formed by its own lane: the f32 box-test constants, the flags, and
-// whether the ray is walked at all (YART_COOP_CULL). A ray whose conservative test misses the
+// whether the ray is walked at all (the cull box). A ray whose conservative test misses the
 // mesh's cull box (the union of both roots' child boxes) is left out of the walk: every child box
 // of either root lies inside that box, the f32 test passes on a box whenever it passes on a box
 // inside it (the fma bounds are monotone in the corners) and whenever the reference's f64 test
@@ -1030,7 +935,6 @@ __device__ __forceinline__ CoopStage coop_stage(const DevMesh& M, bool has_aux, 
   }
   s.flags = (ok ? 1u : 0u) | (ray_octant(sdir) << 1);
   s.walk = true;
-#if YART_COOP_CULL
   if (ok) {
     const vfloat2 cc[3] = {vfloat2{s.c32[0], s.c32[1]}, vfloat2{s.c32[2], s.c32[3]}, vfloat2{s.c32[4], s.c32[5]}};
     const float4 blo = make_float4(M.box_lo[0], M.box_lo[1], M.box_lo[2], M.box_lo[3]);
@@ -1038,7 +942,6 @@ __device__ __forceinline__ CoopStage coop_stage(const DevMesh& M, bool has_aux, 
     float ent;
     s.walk = child_hit_f32(blo, bhi, s.inv32, cc, tmin32, (float)(tmax + fabs(tmax) * 0x1p-20), ent);
   }
-#endif
   return s;
 }
 __device__ __forceinline__ void coop_write(CoopRay& s, const Ray& r, double tmax, const CoopStage& g) {
@@ -1069,8 +972,9 @@ __device__ __forceinline__ bool coop_check(const __attribute__((address_space(1)
   }
   return h > l && t >= l;
 }
+// Inlined: +4 % david, +11 % bunny over a call (the call site spills the caller's state).
 template <bool STATS, int SLOTS = kCoopSlots>
-__device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
+__device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
                                        uint8_t* __restrict__ lds, Stats& st) {
   found = false;
@@ -1097,9 +1001,9 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
   uint32_t ray = q, next = 16;
-  // YART_COOP_POSTCHECK: W's exact check after the walk, per lane (the 32-slot walks only: the
-  // per-lane re-walk, qbvh_t, has a 32-slot stack)
-  constexpr bool kPostCheck = YART_COOP_POSTCHECK && SLOTS == kCoopSlots;
+  // W's exact check after the walk, per lane (the 32-slot walks only: the per-lane re-walk,
+  // qbvh_t, has a 32-slot stack; the 64-slot walks check W where the ray's walk ends)
+  constexpr bool kPostCheck = SLOTS == kCoopSlots;
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
   double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
@@ -1147,16 +1051,7 @@ __device__ YART_COOP_ATTR void qbvh_coop(const DevMesh& M, bool want, const Ray&
       }
     }
     bool fin = false;
-#if YART_COOP_LEAF_MIN > 1
-    // Leaf rounds wait until enough quads sit at a leaf (or none can descend): a round pays for
-    // each branch any quad takes, and the leaf branch is the expensive one.
-    const uint64_t at_leaf = __ballot(has && c == 0 && (node >> 31));
-    const uint64_t at_inner = __ballot(has && c == 0 && !(node >> 31));
-    const bool leaf_round = __popcll(at_leaf) >= YART_COOP_LEAF_MIN || at_inner == 0;
-#else
-    const bool leaf_round = true;
-#endif
-    if (has && (leaf_round || !(node >> 31))) {  // quad-uniform from here on
+    if (has) {  // quad-uniform from here on
       bool popped = false;  // the inner step set the next node itself
       if (node >> 31) {
         uint32_t count = (node >> 27) & 0xFu;
@@ -1364,10 +1259,6 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 // ------------------------------------------------------------------------ world hit
 // Which primitive of the world list won, and where: enough to rebuild its record exactly.
 struct HitId { double t, u, v; uint32_t obj, sub; };
-// What the world pass captured for the light-pdf slots (device_types.h kMaxLpf).
-// The t's go to LDS (the lane's column of a [slot][lane] array): held in registers across the
-// world pass they pushed the list kernel into spilling inside its object loop (-12 %).
-struct LightCap { double* t; bool hit[kMaxLpf]; };
 
 template <bool HAS_MESH, bool STATS>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
@@ -1440,8 +1331,6 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // dead-but-compiled code: registers and spills).
 // HAS_MESH: called from converged code by all 64 lanes, `want` marking the lanes with a query —
 // meshes are walked cooperatively (qbvh_coop) by the whole wave, the other objects per lane.
-// LPF: objects holding a light-pdf slot are tested with the capture forms (rect_t_cap /
-// sphere_t_cap: the same t and answer as prim_t, plus the [t_min, inf) test pdf_value makes).
 // A wave-uniform read of a scene table (the list walk's object, a light of the mixture pdf): the
 // index made uniform by readfirstlane and the table read through the constant address space, so
 // the record arrives by scalar loads into SGPRs. Read as a plain global, the loads after the
@@ -1449,18 +1338,13 @@ __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, 
 // field of the record took a VGPR.
 template <class T>
 __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
-#ifdef YART_VECTOR_SCENE
-  return base[i];
-#else
   typedef const __attribute__((address_space(4))) T* cptr;
   return *(const T*)((cptr)base + __builtin_amdgcn_readfirstlane(i));
-#endif
 }
 
-template <bool HAS_MESH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
+template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
-                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                              LightCap* cap = nullptr) {
+                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
   bool found = false;
   double closest = tmax;
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -1483,24 +1367,8 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       const Ray lr = to_local(o, nxf, r);
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
-      bool hit = false;
-      if (LPF && o.lpf < kMaxLpf) {  // wave-uniform; no wrapper but FlipFace: lr is r
-        if (STATS) st.v[ST_PRIM]++;
-#pragma unroll
-        for (uint32_t k = 0; k < kMaxLpf; ++k) {
-          if (o.lpf == k) {
-            if (kind == YART_PRIM_SPHERE) {
-              hit = sphere_t_cap(o.p, lr, tmin, closest, t, cap->hit[k]);
-            } else {
-              hit = rect_t_cap<1, 0, 2>(o.p, lr, tmin, closest, t, cap->hit[k]);
-              cap->t[k * 64] = t;
-            }
-          }
-        }
-      } else {
-        hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                     : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
-      }
+      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1571,9 +1439,6 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
 // (~1e-7 relative) stays far inside m — over [t_min, closest] widened by 2^-10, so it never
 // drops a node holding a hit the scan would accept (ties included). Non-finite rays take the
 // list walk.
-#ifndef YART_WORLD_SPH
-#define YART_WORLD_SPH 1
-#endif
 template <bool STATS>
 __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
                                                   uint32_t* stk, Stats& st) {
@@ -1601,7 +1466,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   for (;;) {
     const uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
     bool pop = true;
-    if (count && YART_WORLD_SPH && ((hnd >> 27) & 1u)) {
+    if (count && ((hnd >> 27) & 1u)) {
       // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
       // object records and the kind switch; the same sphere_t on the same values
       for (uint32_t k = 0; k < count; ++k) {
@@ -1674,15 +1539,14 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, bool LPF = false, int SLOTS = kCoopSlots>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, int SLOTS = kCoopSlots>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                          LightCap* cap = nullptr) {
+                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, LPF, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q, cap) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -1959,233 +1823,135 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
-#ifndef YART_WAVES_PER_EU
-#define YART_WAVES_PER_EU 4  // 128 VGPRs -> 4 waves per SIMD (+5% over 3 on the cornell box)
-#endif
-// DYN (chunked path only): the unit's 64 pixels x `chunk` samples form a job list that the wave's
-// lanes pull from dynamically — a lane whose path ends takes the next (pixel, sample) job, the
-// wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
-// no lane idles while another still has samples of its own pixel left. Safe because each
-// (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
-#ifndef YART_MESH_WAVES_PER_EU
-#define YART_MESH_WAVES_PER_EU 4  // 128 VGPRs; traversal is latency-bound: +36% on david over 2
-#endif
-// Lane-occupancy probe (debug builds with -DYART_OCC only, tools/occupancy.py): per region, the
-// number of wave executions and the lanes active in them.
-enum { OCC_ITER, OCC_FRESH, OCC_LAMB, OCC_LAMB_LIGHT, OCC_LAMB_COS, OCC_DIEL, OCC_METAL, OCC_WALK, OCC_TERM, OCC_ASSIGN };
-#ifdef YART_OCC
-__device__ unsigned long long g_occ[32];
-#define OCC(k)                                                                         \
-  do {                                                                                 \
-    const uint64_t m_ = __ballot(1);                                                   \
-    if (lane == (uint32_t)__builtin_ctzll(m_)) {                                       \
-      atomicAdd(&g_occ[2 * (k)], 1ull);                                                \
-      atomicAdd(&g_occ[2 * (k) + 1], (unsigned long long)__popcll(m_));                \
-    }                                                                                  \
-  } while (0)
-#else
-#define OCC(k) do {} while (0)
-#endif
-// Cycle probe (debug builds with -DYART_PROF only, tools/cycles.py): the shader clock (s_memtime)
-// around each region; whichever lanes run it, the first active lane adds the region's cycles to its
-// wave's LDS counter (a divergent region is timed once per wave execution), and the waves' counters
-// are added into g_prof at exit. Regions nest (the material branches sit inside PF_SCATTER).
-enum { PF_LOOP, PF_ASSIGN, PF_RNG, PF_CAMERA, PF_SCATTER, PF_LAMB, PF_METAL, PF_DIEL, PF_WORLD, PF_SHADE, PF_TERM,
-       PF_WAVES, PF_N };
-#ifdef YART_PROF
-__device__ unsigned long long g_prof[16];
-__shared__ unsigned long long s_prof[4 * PF_N];
-struct ProfScope {
-  int k;
-  uint64_t t0;
-  __device__ explicit ProfScope(int k_) : k(k_), t0(__builtin_amdgcn_s_memtime()) {}
-  __device__ ~ProfScope() {
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
-    if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)))
-      atomicAdd(&s_prof[(threadIdx.x >> 6) * PF_N + k], (unsigned long long)(t1 - t0));
-  }
-};
-#define PROF_CAT2(a, b) a##b
-#define PROF_CAT(a, b) PROF_CAT2(a, b)
-#define PROF(k) const ProfScope PROF_CAT(prof_, __LINE__)(k)
-#else
-#define PROF(k) do {} while (0)
-#endif
-// Marginal-cost probe (debug builds with -DYART_DUP=k only, tools/dup_cost.py): region k (1 camera,
-// 2 scatter, 3 world pass, 4 sample end, 5 the iteration's Philox blocks) runs g_dup times per
-// execution, its inputs and outputs laundered so the repeats are neither merged nor dead; the frame
-// time's slope in g_dup is what one execution of the region costs the kernel.
-#ifdef YART_DUP
-__device__ uint32_t g_dup = 1;
-#define DUP_LOOP(k) for (uint32_t dup_i = 0, dup_n = (YART_DUP == (k) ? __builtin_amdgcn_readfirstlane(g_dup) : 1u); dup_i < dup_n; ++dup_i)
-#define DUP_LAUNDER(x) asm volatile("" : "+v"(x))
-#else
-#define DUP_LOOP(k)
-#define DUP_LAUNDER(x) do {} while (0)
-#endif
+// Waves per SIMD: 128 VGPRs -> 4 (+5 % over 3 on the cornell box; traversal is latency-bound:
+// +36 % on david over 2, and 3 or 5 lose on every kernel).
+constexpr int kWavesPerEu = 4;
+constexpr int kMeshWavesPerEu = 4;
 
 // Material::scatter at the stored hit + the mixture pdf (material.rs, main.rs:548-584): the path's
 // next ray and throughput, or its end. One body for both math policies (the Fast cores first; a
 // lane whose operand left a core's range re-runs it on the IEEE sequences from the same inputs
 // and the same draws) and for both render paths (k_render's fused loop, k_wf_shade).
-template <bool EXT, bool STATS, bool LPF, class MP>
+template <bool EXT, bool STATS, class MP>
 __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, const V3& hp, const V3& hn, uint32_t hmat,
                                            double hu, double hv, int wbin, const Ray& ray, double T, uint32_t depth,
                                            Stats& st, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_,
-                                           bool& term_, double& Tp_, double& cosv_, bool& pend_) {
-#ifdef YART_OCC
-  const uint32_t lane = __lane_id();
-#endif
-    T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false; pend_ = false;
-    const DevMaterial& m = S.materials[hmat];
-    const uint32_t kind = m.kind;
-    if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
-      OCC(OCC_LAMB);
-      PROF(PF_LAMB);
-      // the albedo is looked up where it is multiplied in: fetched here, it was held (and
-      // spilled) through the direction sampling and the light pdfs
-      auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
-      const Onb uvw = onb_from_w(hn, mp);
-      V3 dir;
-      double pdf_val;
-      if (S.n_lights == 0) {
-        (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
-        dir = local(uvw, random_cosine_direction(g, mp));
-        pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
-      } else {
-        if (gen_range(g, 0.0, 1.0) < 0.5) {
-          // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
-          OCC(OCC_LAMB_LIGHT);
-#ifndef YART_LIGHT_K_LANE
-          if (S.n_lights <= 2) {  // k = 0 for every lane (gen_index(g, 1) draws nothing): scalar loads
-            dir = light_random(uniform_at(S.lights, 0u), hp, g, mp);
-          } else {
-            const uint32_t k = (uint32_t)gen_index(g, S.n_lights - 1);
-            dir = light_random(S.lights[k], hp, g, mp);
-          }
-#else
-          const uint32_t k = S.n_lights == 1 ? 0u : (uint32_t)gen_index(g, S.n_lights - 1);
+                                           bool& term_) {
+  T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false;
+  const DevMaterial& m = S.materials[hmat];
+  const uint32_t kind = m.kind;
+  if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
+    // the albedo is looked up where it is multiplied in: fetched here, it was held (and
+    // spilled) through the direction sampling and the light pdfs
+    auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
+    const Onb uvw = onb_from_w(hn, mp);
+    V3 dir;
+    double pdf_val;
+    if (S.n_lights == 0) {
+      (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
+      dir = local(uvw, random_cosine_direction(g, mp));
+      pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
+    } else {
+      if (gen_range(g, 0.0, 1.0) < 0.5) {
+        // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
+        if (S.n_lights <= 2) {  // k = 0 for every lane (gen_index(g, 1) draws nothing): scalar loads
+          dir = light_random(uniform_at(S.lights, 0u), hp, g, mp);
+        } else {
+          const uint32_t k = (uint32_t)gen_index(g, S.n_lights - 1);
           dir = light_random(S.lights[k], hp, g, mp);
-#endif
-        } else {
-          OCC(OCC_LAMB_COS);
-          dir = local(uvw, random_cosine_direction(g, mp));
         }
-        if (LPF && S.n_lpf != 0) {  // finished after the world pass (resolve)
-          pdf_val = 0.0;
-          cosv_ = cosine_value(uvw, dir, mp);
-          pend_ = true;
-        } else {
-          const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
-          double sum = -0.0;
-          for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ray.wl, st, mp);
-          pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
-        }
-      }
-      if (pend_) {
-        const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
-        const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-        Tp_ = (T * att()) * spdf;
-        o_ = hp;
-        d_ = dir;
-        depth_ = depth - 1;
-      } else if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-        R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-        term_ = true;
       } else {
-        const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
-        const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
-        T_ = ((T * att()) * spdf) / pdf_val;
-        o_ = hp;
-        d_ = dir;
-        depth_ = depth - 1;
+        dir = local(uvw, random_cosine_direction(g, mp));
       }
-    } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
-      const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
-      V3 p;
-      for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-        const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-        p = mk(px, py, pz);
-        if (!(len2(p) >= 1.0)) break;
-      }
-      T_ = T * att;
+      const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+      double sum = -0.0;
+      for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ray.wl, st, mp);
+      pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
+    }
+    if (!isfinite(pdf_val) || pdf_val <= 0.0) {
+      R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
+      term_ = true;
+    } else {
+      const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+      const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+      T_ = ((T * att()) * spdf) / pdf_val;
       o_ = hp;
-      d_ = p;
-      depth_ = depth - 1;
-    } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
-      OCC(OCC_METAL);
-      PROF(PF_METAL);
-      const V3 reflected = reflect(mp.unit(ray.d), hn);
-      V3 p;
-      for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
-        const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
-        p = mk(px, py, pz);
-        if (!(len2(p) >= 1.0)) break;
-      }
-      const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
-      T_ = T * att;
-      o_ = hp;
-      d_ = add(reflected, smul(m.fuzz, p));
-      depth_ = depth - 1;
-    } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
-      OCC(OCC_DIEL);
-      PROF(PF_DIEL);
-      const double wl2 = ray.wl * ray.wl;
-      const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
-      const double n = mp.sqrt(n2);
-      // |d| divides the incidence cosine and, in unit_vector(d), the three components
-      const PosDen ld = mp.den(mp.len(ray.d));
-      V3 outward;
-      double ni_over_nt, cosine;
-      if (dot(ray.d, hn) > 0.0) {
-        outward = neg(hn); ni_over_nt = n; cosine = mp.quo(n * dot(ray.d, hn), ld);
-      } else {
-        outward = hn; ni_over_nt = 1.0 / n; cosine = mp.quo(-dot(ray.d, hn), ld);
-      }
-      const V3 uv = mk(mp.quo(ray.d.x, ld), mp.quo(ray.d.y, ld), mp.quo(ray.d.z, ld));  // refract (material.rs:195-205)
-      const double dt = dot(uv, outward);
-      const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
-      V3 out;
-      if (disc > 0.0) {
-        const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, mp.sqrt(disc)));
-        double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
-        r0 = r0 * r0;
-        const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
-        out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
-      } else {
-        out = reflect(ray.d, hn);
-      }
-      T_ = T * 1.0;
-      o_ = hp;
-      d_ = out;
+      d_ = dir;
       depth_ = depth - 1;
     }
+  } else if (EXT && kind == YART_MAT_ISOTROPIC) {  // material.rs:370-381: a specular-type scatter
+    const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
+    V3 p;
+    for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+      const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+      p = mk(px, py, pz);
+      if (!(len2(p) >= 1.0)) break;
+    }
+    T_ = T * att;
+    o_ = hp;
+    d_ = p;
+    depth_ = depth - 1;
+  } else if (kind == YART_MAT_METAL) {  // material.rs:79-95
+    const V3 reflected = reflect(mp.unit(ray.d), hn);
+    V3 p;
+    for (int guard = 0; guard < 1024; ++guard) {  // random_in_unit_sphere material.rs:308-324
+      const double px = gen_range(g, -1.0, 1.0), py = gen_range(g, -1.0, 1.0), pz = gen_range(g, -1.0, 1.0);
+      p = mk(px, py, pz);
+      if (!(len2(p) >= 1.0)) break;
+    }
+    const double att = texture_value<EXT>(S, m.texture, wbin, hp, hu, hv);
+    T_ = T * att;
+    o_ = hp;
+    d_ = add(reflected, smul(m.fuzz, p));
+    depth_ = depth - 1;
+  } else {  // YART_MAT_DIELECTRIC, material.rs:213-301
+    const double wl2 = ray.wl * ray.wl;
+    const double n2 = 1.0 + m.b[0] * wl2 / (wl2 - m.c[0]) + m.b[1] * wl2 / (wl2 - m.c[1]) + m.b[2] * wl2 / (wl2 - m.c[2]);
+    const double n = mp.sqrt(n2);
+    // |d| divides the incidence cosine and, in unit_vector(d), the three components
+    const PosDen ld = mp.den(mp.len(ray.d));
+    V3 outward;
+    double ni_over_nt, cosine;
+    if (dot(ray.d, hn) > 0.0) {
+      outward = neg(hn); ni_over_nt = n; cosine = mp.quo(n * dot(ray.d, hn), ld);
+    } else {
+      outward = hn; ni_over_nt = 1.0 / n; cosine = mp.quo(-dot(ray.d, hn), ld);
+    }
+    const V3 uv = mk(mp.quo(ray.d.x, ld), mp.quo(ray.d.y, ld), mp.quo(ray.d.z, ld));  // refract (material.rs:195-205)
+    const double dt = dot(uv, outward);
+    const double disc = 1.0 - ni_over_nt * ni_over_nt * (1.0 - dt * dt);
+    V3 out;
+    if (disc > 0.0) {
+      const V3 refracted = sub(muls(sub(uv, muls(outward, dt)), ni_over_nt), muls(outward, mp.sqrt(disc)));
+      double r0 = (1.0 - n) / (1.0 + n);  // schlick (material.rs:207-211)
+      r0 = r0 * r0;
+      const double sch = r0 + (1.0 - r0) * powi5(1.0 - cosine);
+      out = gen_f64(g) < sch ? reflect(ray.d, hn) : refracted;
+    } else {
+      out = reflect(ray.d, hn);
+    }
+    T_ = T * 1.0;
+    o_ = hp;
+    d_ = out;
+    depth_ = depth - 1;
+  }
 }
 
-#ifndef YART_REGEN_MIN
-#define YART_REGEN_MIN 1
-#endif
-#ifndef YART_LPF
-#define YART_LPF 0
-#endif
-#ifndef YART_JOBL
-#define YART_JOBL 1
-#endif
+// DYN (chunked path only): the unit's 64 pixels x `chunk` samples form a job list that the wave's
+// lanes pull from dynamically — a lane whose path ends takes the next (pixel, sample) job, the
+// wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
+// no lane idles while another still has samples of its own pixel left. Safe because each
+// (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
-__global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES_PER_EU) void k_render(DevScene S, RenderArgs A) {
+__global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void k_render(DevScene S, RenderArgs A) {
   __shared__ uint32_t s_stack[HAS_MESH ? 4 * kWaveLdsWords : BVH ? 4 * kStackSlots * 64 : 1];
-  // LPF (build with -DYART_LPF=1): the list kernels capture light hits in the world pass. Off by
-  // default — bitwise either way, but measured slower: cornell 4,174 vs 4,585 Msamples/s (the extra
-  // code in the object loop and the deferred state cost more registers than the re-tests it saves).
-  constexpr bool LPF = YART_LPF && !HAS_MESH && !BVH;
   // JOBL (the chunked list and world-BVH kernels): a lane's job identity — pixel, sample, block, slot, x, y —
   // lives in LDS ([word][lane] per wave) from its hand-out to its scratch store, read where it is
   // used, instead of six VGPRs carried through every iteration.
   // The mesh kernel's LDS is nearly full (36.9 KB of walk state per workgroup): it keeps three
   // words (pixel, sample, block) and derives x, y and the slot from the pixel where needed.
-  constexpr bool JOBL = YART_JOBL && DYN && !HAS_MESH, JOBL3 = YART_JOBL && DYN && HAS_MESH;
+  constexpr bool JOBL = DYN && !HAS_MESH, JOBL3 = DYN && HAS_MESH;
   __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : JOBL3 ? 4 * 3 * 64 : 1];
-  __shared__ double s_lpf[LPF ? 4 * 4 * 64 : 1];  // per wave [Tp, cosv, t0, t1][lane]
   // the wave index through readfirstlane: uniform, so the per-wave LDS bases live in SGPRs (as a
   // VGPR the mesh walk's stack base was spilled and reloaded at every pop)
   const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2204,7 +1970,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   uint32_t x = bx0 + (slot & 7u), y = by0 + (slot >> 3);
   const uint32_t W = A.width, H = A.height;
   const bool active = x < W && y < H && covered(x, W) && covered(y, H);
-  double* const lpf_lds = &s_lpf[LPF ? wave * 256 + lane : 0];
   uint32_t* const jl = &s_job[JOBL ? wave * 6 * 64 + lane : JOBL3 ? wave * 3 * 64 + lane : 0];
   constexpr bool JL = JOBL || JOBL3;
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
@@ -2235,25 +2000,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
   double hu = 0.0, hv = 0.0;            // its texture coordinates (EXT)
   int wbin = 0;                         // spectrum bin of the path's wavelength
   g.k0 = (uint32_t)A.seed; g.k1 = (uint32_t)(A.seed >> 32);
-#ifdef YART_PROF
-  if (lane < PF_N) s_prof[wave * PF_N + lane] = 0ull;
-#endif
 
   // The loop exits wave-uniformly: a lane without work stays in it with `run` false, so the
   // mesh walk (qbvh_coop) is reached by all 64 lanes together.
   for (;;) {
-    PROF(PF_LOOP);
     if (DYN) {
-      PROF(PF_ASSIGN);
       uint64_t m = drained ? 0ull : __ballot(need);
-#if YART_REGEN_MIN > 1
-      // Regeneration threshold (A/B flag): lanes whose path ended wait, idle, until at least
-      // YART_REGEN_MIN of them ask (or no lane of the wave is still running), so the camera block
-      // runs for more lanes at once. Invariant: every draw is keyed by (pixel, sample, phase).
-      if (m && __popcll(m) < YART_REGEN_MIN && __ballot(!need) != 0ull) m = 0ull;
-#endif
       while (m) {  // wave-uniform: hand out jobs until every asking lane has one
-        OCC(OCC_ASSIGN);
         if (next_job >= n_jobs) {  // claim the next unit
           const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
           uint32_t v = 0;
@@ -2302,65 +2055,12 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     if (__ballot(run) == 0) break;
     double R = 0.0;
     bool term = false, want = false;
-    // LPF: a Lambertian scatter's mixture pdf waits for the world pass of the ray it sampled,
-    // which captures the light hits pdf_value would re-test (device_types.h kMaxLpf): T·att·spdf
-    // (Tp) and the cosine half (cosv) are kept until then, T stays the incoming throughput.
-    bool pend = false;
-    double* const Tp = &lpf_lds[0], * const cosv = &lpf_lds[64];  // LDS, [value][lane]
-    // Every light whose pdf_value intersects holds a slot (capi.cpp assign_lpf: all or none); the
-    // others' pdf_value is 0 (hittable.rs:28-30).
-    auto resolve = [&](const LightCap& c) {  // hittable.rs:103-111 + pdf.rs mixture, material.rs:56-60
-      Ieee im;
-      const double weight = 1.0 / (double)S.n_lights;
-      double sum = -0.0;
-      for (uint32_t i = 0; i < S.n_lights; ++i) {
-        const DevObject& L = uniform_at(S.lights, i);
-        double v = 0.0;
-        if (L.lpf < kMaxLpf) {  // wave-uniform
-          if (STATS) st.v[ST_LIGHT]++;
-          bool h = false;
-          double t = 0.0;
-#pragma unroll
-          for (uint32_t k = 0; k < kMaxLpf; ++k)
-            if (L.lpf == k) { h = c.hit[k]; t = c.t[k * 64]; }
-          v = light_pdf_at(L, ray.o, ray.d, h, t, im);
-        }
-        sum = sum + weight * v;
-      }
-      const double pdf_val = 0.5 * sum + 0.5 * *cosv;
-      pend = false;
-      if (!isfinite(pdf_val) || pdf_val <= 0.0) {
-        R = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
-        term = true;
-      } else {
-        T = *Tp / pdf_val;
-      }
-    };
     if (run) {
-      OCC(OCC_ITER);
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
-      {
-        PROF(PF_RNG);
-        DUP_LOOP(5) {
-        DUP_LAUNDER(g.k0);
-        rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
-        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3);
-        DUP_LAUNDER(g.b4); DUP_LAUNDER(g.b5); DUP_LAUNDER(g.b6); DUP_LAUNDER(g.b7);
-        }
-      }
+      rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, fresh ? 0u : A.max_depth - depth + 1u);
       if (fresh) {  // main.rs:692-698
-        OCC(OCC_FRESH);
-        PROF(PF_CAMERA);
-#ifdef YART_DUP
-        const Rng g_dup0 = g;
-#endif
-        DUP_LOOP(1) {
-#ifdef YART_DUP
-        g = g_dup0;
-        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3);
-#endif
         uint32_t jx = x, jy = y;
         if (JOBL) { jx = jl[256]; jy = jl[320]; }
         if (JOBL3) { const uint32_t p = jl[0]; jy = p / W; jx = p - jy * W; }
@@ -2369,60 +2069,35 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         const double ty = (double)jy + gen_f64(g);
         const double v = 1.0 - ty / (double)(H - 1);
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
-#ifndef YART_NO_LAUNDER
         ray = camera_ray(*kernarg_camera(), u, v, wl, g, EXT && S.has_time);
         wbin = spectrum_bin(wl);  // the path's reflectance bin (color.rs:276-283), once per sample
-#else
-        ray = camera_ray(A.cam, u, v, wl, g, EXT && S.has_time);
-        wbin = spectrum_bin(wl);
-#endif
-        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.o.y); DUP_LAUNDER(ray.o.z);
-        DUP_LAUNDER(ray.d.x); DUP_LAUNDER(ray.d.y); DUP_LAUNDER(ray.d.z); DUP_LAUNDER(ray.wl); DUP_LAUNDER(wbin);
-        }
         T = 1.0;
         depth = A.max_depth;
         fresh = false;
       } else {  // scatter at the stored hit (material.rs), main.rs:548-584
-        PROF(PF_SCATTER);
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
-        auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_,
-                           double& Tp_, double& cosv_, bool& pend_) {
-          scatter_at<EXT, STATS, LPF>(S, mp, g, hp, hn, hmat, hu, hv, wbin, ray, T, depth, st, T_, o_, d_, depth_, R_,
-                                      term_, Tp_, cosv_, pend_);
+        auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_) {
+          scatter_at<EXT, STATS>(S, mp, g, hp, hn, hmat, hu, hv, wbin, ray, T, depth, st, T_, o_, d_, depth_, R_, term_);
         };
-        double nT, nR, nTp = 0.0, ncosv = 0.0;
+        double nT, nR;
         V3 no, nd;
         uint32_t ndepth;
-        bool nterm, npend;
+        bool nterm;
         typename MathPolicy<HAS_MESH, BVH, EXT>::type fm;
-#ifdef YART_DUP
-        const Rng g_dup0 = g;
-        DUP_LOOP(2) {
-        g = g_dup0;
-        DUP_LAUNDER(g.b0); DUP_LAUNDER(g.b1); DUP_LAUNDER(g.b2); DUP_LAUNDER(g.b3); DUP_LAUNDER(T);
-        fm = typename MathPolicy<HAS_MESH, BVH, EXT>::type{};
-        scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
-        DUP_LAUNDER(nT); DUP_LAUNDER(no.x); DUP_LAUNDER(no.y); DUP_LAUNDER(no.z); DUP_LAUNDER(nd.x); DUP_LAUNDER(nd.y);
-        DUP_LAUNDER(nd.z); DUP_LAUNDER(nR); DUP_LAUNDER(ndepth);
-        }
-#else
-        scatter(fm, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
-#endif
+        scatter(fm, nT, no, nd, ndepth, nR, nterm);
         if (flagged(fm)) {  // rare: the same draws again, on the IEEE sequences
           rng_phase<!HAS_MESH && !BVH>(g, JL ? jl[0] : pixel, JL ? jl[64] : smp, A.max_depth - depth + 1u);
           Ieee im;
-          scatter(im, nT, no, nd, ndepth, nR, nterm, nTp, ncosv, npend);
+          scatter(im, nT, no, nd, ndepth, nR, nterm);
         }
         T = nT; ray.o = no; ray.d = nd; depth = ndepth; R = nR; term = nterm;
-        pend = npend;
-        if (LPF && pend) { *Tp = nTp; *cosv = ncosv; }
       }
       if (!term) {
-        if (depth == 0 && !(LPF && pend)) {  // main.rs:544-546: exhausted depth reflects 1.0
+        if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
           R = T * 1.0;
           term = true;
-        } else {  // (a pending pdf at depth 0 is finished by the world pass's capture, below)
+        } else {
           want = true;
         }
       }
@@ -2431,35 +2106,14 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       Hit h;
       int32_t which;
       bool hit = false;
-      LightCap cap;
-      cap.t = &lpf_lds[128];
       bool scat = false;
       const QueryCtx q{g.k0, g.k1, JL ? jl[64] : smp, JL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
-        PROF(PF_WORLD);
-        DUP_LOOP(3) {
-        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
-        DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
-        }
       } else if (want) {
-        OCC(OCC_WALK);
-        PROF(PF_WORLD);
-        DUP_LOOP(3) {
-        DUP_LAUNDER(ray.o.x); DUP_LAUNDER(ray.d.x);
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT, LPF>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q, &cap);
-        DUP_LAUNDER(h.t); DUP_LAUNDER(h.p.x); DUP_LAUNDER(h.n.x); DUP_LAUNDER(which);
-        }
-      }
-      if (LPF && want && pend) {
-        resolve(cap);
-        if (!term && depth == 0) {  // the sampled ray was traced only for its light hits
-          R = T * 1.0;
-          term = true;
-        }
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       }
       if (want && !term) {
-        PROF(PF_SHADE);
         if (STATS) st.v[ST_SEGMENTS]++;
         if (!hit) {
           R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
@@ -2487,10 +2141,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
       if (EXT) { hu = scat ? h.u : 0.0; hv = scat ? h.v : 0.0; }
     }
     if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
-      OCC(OCC_TERM);
-      PROF(PF_TERM);
-      DUP_LOOP(4) {
-      DUP_LAUNDER(R); DUP_LAUNDER(ray.wl);
       double cx, cy, cz;
       cie_xyz(ray.wl, cx, cy, cz);
       double sx = cx * R, sy = cy * R, sz = cz * R;
@@ -2509,7 +2159,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
           jsl = (py & 7u) * 8u + (px & 7u);
         }
         double* q = A.scratch + 3 * (((size_t)jb * A.s_count + (js - A.s_begin)) * 64 + jsl);
-        DUP_LAUNDER(sx); DUP_LAUNDER(sy); DUP_LAUNDER(sz);
         q[0] = sx; q[1] = sy; q[2] = sz;
         need = true;
       } else {
@@ -2517,7 +2166,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
         smp++;
         if (smp < s_stop) fresh = true;
         else alive = false;
-      }
       }
     }
   }
@@ -2533,10 +2181,6 @@ __global__ __launch_bounds__(256, HAS_MESH ? YART_MESH_WAVES_PER_EU : YART_WAVES
     for (int i = 0; i < kNumStats; ++i)
       if (st.v[i]) atomicAdd(&A.stats[i], st.v[i]);
   }
-#ifdef YART_PROF
-  if (lane < PF_WAVES) atomicAdd(&g_prof[lane], s_prof[wave * PF_N + lane]);
-  if (lane == 0) atomicAdd(&g_prof[PF_WAVES], 1ull);
-#endif
 }
 
 // ------------------------------------------------------------- wavefront path (mesh scenes)
@@ -2616,13 +2260,12 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
         uint32_t pixel, smp, x, y;
         wf_job(A, job, pixel, smp, x, y);
         rng_phase<false>(g, pixel, smp, A.max_depth - depth + 1u);
-        double nT, nR, nTp = 0.0, ncosv = 0.0;
+        double nT, nR;
         V3 no, nd;
         uint32_t ndepth;
-        bool nterm, npend;
+        bool nterm;
         Ieee im;
-        scatter_at<false, false, false>(S, im, g, h.p, h.n, h.mat, 0.0, 0.0, wbin, ray, T, depth, st, nT, no, nd, ndepth, nR,
-                                        nterm, nTp, ncosv, npend);
+        scatter_at<false, false>(S, im, g, h.p, h.n, h.mat, 0.0, 0.0, wbin, ray, T, depth, st, nT, no, nd, ndepth, nR, nterm);
         if (nterm) {
           R = nR;
           term = true;
@@ -2728,16 +2371,11 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
   if (__syncthreads_or(has) && threadIdx.x == 0) *F.alive = 1u;
 }
 
-#ifndef YART_WF_TRACE_WAVES
-#define YART_WF_TRACE_WAVES 4  // LDS-bound: the cooperative walk's 9.2 KB per wave
-#endif
-#ifndef YART_WF_PERSIST
-#define YART_WF_PERSIST 0
-#endif
+constexpr int kWfTraceWaves = 4;  // LDS-bound: the cooperative walk's 9.2 KB per wave
 // One wave per workgroup: a wave that finishes frees its slot (LDS included) for the next one
 // without waiting for slower waves of a larger workgroup.
 template <int SLOTS>
-__global__ __launch_bounds__(64, SLOTS == kCoopSlots ? YART_WF_TRACE_WAVES : 3) void k_wf_trace(DevScene S, RenderArgs A,
+__global__ __launch_bounds__(64, SLOTS == kCoopSlots ? kWfTraceWaves : 3) void k_wf_trace(DevScene S, RenderArgs A,
                                                                                             WfArgs F) {
   constexpr int kWords = wave_lds_words<SLOTS>();
   __shared__ uint32_t s_stack[kWords];
@@ -2749,9 +2387,9 @@ __global__ __launch_bounds__(64, SLOTS == kCoopSlots ? YART_WF_TRACE_WAVES : 3) 
   const uint32_t lane = threadIdx.x, P = F.pool;
   uint32_t* stk = &s_stack[lane];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[0]);
-  // YART_WF_PERSIST: a resident grid, each wave walking every gridDim-th batch of 64 slots (no
-  // per-launch refill of waves); else one batch per wave.
-  for (uint32_t bt = blockIdx.x; bt < P / 64u; bt += YART_WF_PERSIST ? gridDim.x : P) {
+  // one batch of 64 slots per wave (a resident grid walking every gridDim-th batch was 11-14 %
+  // slower)
+  for (uint32_t bt = blockIdx.x; bt < P / 64u; bt += P) {
     const uint32_t i = bt * 64u + lane;
     const bool want = F.q.job[i] != kWfNoJob;
     if (__ballot(want) == 0) continue;  // wave-uniform: the walk needs the whole wave
@@ -2762,7 +2400,7 @@ __global__ __launch_bounds__(64, SLOTS == kCoopSlots ? YART_WF_TRACE_WAVES : 3) 
     HitId id;
     Stats st;
     const QueryCtx q{0u, 0u, 0u, 0u, 0u};  // no media on this path
-    const bool hit = world_closest<true, false, false, false, SLOTS>(S, want, r, 0.001, INFINITY, id, stk, coop, st, q);
+    const bool hit = world_closest<true, false, false, SLOTS>(S, want, r, 0.001, INFINITY, id, stk, coop, st, q);
     if (want) {
       F.q.ht[i] = id.t; F.q.hu[i] = id.u; F.q.hv[i] = id.v;
       F.q.hobj[i] = hit ? id.obj : kWfMiss;
@@ -2813,7 +2451,7 @@ __global__ __launch_bounds__(256) void k_unpack_shards(const double* __restrict_
 
 // ------------------------------------------------------------------- batched closest hit
 template <int SLOTS>
-__global__ __launch_bounds__(256, SLOTS == kCoopSlots ? YART_MESH_WAVES_PER_EU : 3) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
+__global__ __launch_bounds__(256, SLOTS == kCoopSlots ? kMeshWavesPerEu : 3) void k_intersect(DevScene S, const double* __restrict__ rays, uint32_t n,
                                                    double* __restrict__ hits, int32_t* __restrict__ obj) {
   constexpr int kWords = wave_lds_words<SLOTS>();
   __shared__ uint32_t s_stack[4 * kWords];
@@ -2832,7 +2470,7 @@ __global__ __launch_bounds__(256, SLOTS == kCoopSlots ? YART_MESH_WAVES_PER_EU :
   if (S.world_nodes) {
     if (active) hit = world_hit<false, true, false, false>(S, true, r, q[6], q[7], h, which, stk, coop, st, qc);
   } else {
-    hit = world_hit<true, false, false, true, false, SLOTS>(S, active, r, q[6], q[7], h, which, stk, coop, st, qc);
+    hit = world_hit<true, false, false, true, SLOTS>(S, active, r, q[6], q[7], h, which, stk, coop, st, qc);
   }
   if (!active) return;
   double* o = hits + 8 * (size_t)i;
@@ -2955,7 +2593,7 @@ hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs&
 }
 hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
   const uint32_t batches = w.pool / 64;
-  const uint32_t grid = YART_WF_PERSIST ? (w.resident < batches ? w.resident : batches) : batches;
+  const uint32_t grid = batches;
   if (s.deep) hipLaunchKernelGGL(k_wf_trace<kDeepSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
   else hipLaunchKernelGGL(k_wf_trace<kCoopSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
   return hipGetLastError();
@@ -2991,31 +2629,6 @@ hipError_t launch_probe_math(int op, const double* a, const double* b, uint32_t 
 }
 
 }  // namespace yart_dev
-
-#ifdef YART_OCC
-extern "C" int yart_debug_occupancy(int device, unsigned long long* out32) {
-  if (hipSetDevice(device) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(yart_dev::g_occ), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long z[32] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_occ), z, sizeof z) == hipSuccess ? 0 : -1;
-}
-#endif
-
-#ifdef YART_PROF
-extern "C" int yart_debug_cycles(int device, unsigned long long* out16) {  // reads and clears g_prof
-  if (hipSetDevice(device) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(yart_dev::g_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  unsigned long long z[16] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_prof), z, sizeof z) == hipSuccess ? 0 : -1;
-}
-#endif
-
-#ifdef YART_DUP
-extern "C" int yart_debug_set_dup(int device, unsigned int n) {
-  if (hipSetDevice(device) != hipSuccess) return -1;
-  return hipMemcpyToSymbol(HIP_SYMBOL(yart_dev::g_dup), &n, sizeof n) == hipSuccess ? 0 : -1;
-}
-#endif
 
 extern "C" int yart_debug_force_rewalk(int device, int on) {
   if (hipSetDevice(device) != hipSuccess) return -1;

@@ -148,6 +148,7 @@ struct MultiSlot {
   size_t recv_bytes = 0;
   // devices[0]: the root's gather + unpack interval of each frame not yet read (timing)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_events;
+  uint64_t last_use = 0;              // submission number of its latest frame (eviction order)
 };
 
 struct yart_multi {
@@ -156,35 +157,41 @@ struct yart_multi {
   std::vector<yart_scene*> scenes;
   std::vector<yart_comm*> comms;
   std::mutex mu;                                   // submissions are enqueued one at a time
-  std::map<hipStream_t, std::unique_ptr<MultiSlot>> slots;  // by caller stream (devices[0])
+  std::map<hipStream_t, std::unique_ptr<MultiSlot>> slots;  // by caller stream (devices[0]), at most kMaxSlots
+  uint64_t submissions = 0;
   std::vector<hipEvent_t> last_gather;             // per device: the latest submission's gather
   hipStream_t host_stream = nullptr;               // devices[0]: yart_render_multi's caller stream
   double* frame = nullptr;                         // devices[0]: yart_render_multi's frame
   size_t frame_bytes = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_pool;  // devices[0]: recycled timing pairs
   double render_ms = 0.0, gather_ms = 0.0;  // yart_render_multi's last frame
-  ~yart_multi() {
+  // Drains a slot's streams and frees what it holds (the destructor; eviction of the least recently
+  // used slot when a new caller stream would exceed kMaxSlots, so a caller that makes a stream per
+  // frame does not grow device memory without bound — ADVICE r03).
+  void release_slot(MultiSlot& s) {
     for (int d = 0; d < n && d < (int)devices.size(); ++d) {
       (void)hipSetDevice(devices[(size_t)d]);
-      for (auto& kv : slots) {
-        MultiSlot& s = *kv.second;
-        if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamSynchronize(s.streams[(size_t)d]);
-      }
+      if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamSynchronize(s.streams[(size_t)d]);
     }
     for (int d = 0; d < n && d < (int)devices.size(); ++d) {
       (void)hipSetDevice(devices[(size_t)d]);
-      for (auto& kv : slots) {
-        MultiSlot& s = *kv.second;
-        if ((size_t)d < s.packed.size() && s.packed[(size_t)d]) (void)hipFree(s.packed[(size_t)d]);
-        if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
-        if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamDestroy(s.streams[(size_t)d]);
-        if (d == 0) {
-          for (auto& e : s.gather_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
-          if (s.recv) (void)hipFree(s.recv);
-          if (s.start) (void)hipEventDestroy(s.start);
-          if (s.done) (void)hipEventDestroy(s.done);
-        }
+      if ((size_t)d < s.packed.size() && s.packed[(size_t)d]) (void)hipFree(s.packed[(size_t)d]);
+      if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
+      if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamDestroy(s.streams[(size_t)d]);
+      if (d == 0) {
+        for (auto& e : s.gather_events) gather_pool.push_back(e);  // unread timings are dropped
+        s.gather_events.clear();
+        if (s.recv) (void)hipFree(s.recv);
+        if (s.start) (void)hipEventDestroy(s.start);
+        if (s.done) (void)hipEventDestroy(s.done);
       }
+    }
+    s = MultiSlot{};
+  }
+  ~yart_multi() {
+    for (auto& kv : slots) release_slot(*kv.second);
+    for (int d = 0; d < n && d < (int)devices.size(); ++d) {
+      (void)hipSetDevice(devices[(size_t)d]);
       if (d == 0) {
         for (auto& e : gather_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
         if (frame) (void)hipFree(frame);
@@ -204,8 +211,18 @@ struct RestoreDevice {
   ~RestoreDevice() { (void)hipSetDevice(d); }
 };
 
-// The slot of a caller stream, created on first use (streams and events made once, reused).
+// The slot of a caller stream, created on first use (streams and events made once, reused). At
+// most kMaxSlots live at once: a new caller stream beyond that takes the place of the least
+// recently used slot, after that slot's frames have finished (its streams are drained).
+constexpr size_t kMaxSlots = 8;
 int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
+  if (!m->slots.count(caller) && m->slots.size() >= kMaxSlots) {
+    auto lru = m->slots.begin();
+    for (auto it = m->slots.begin(); it != m->slots.end(); ++it)
+      if (it->second->last_use < lru->second->last_use) lru = it;
+    m->release_slot(*lru->second);
+    m->slots.erase(lru);
+  }
   auto& e = m->slots[caller];
   if (!e) {
     auto s = std::make_unique<MultiSlot>();
@@ -224,6 +241,7 @@ int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
     }
     e = std::move(s);
   }
+  e->last_use = ++m->submissions;
   *out = e.get();
   return YART_OK;
 }

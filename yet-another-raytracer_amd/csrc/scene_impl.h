@@ -14,6 +14,7 @@
 
 namespace yart_impl {
 
+int64_t opt(int option);  // yart_debug_set_option's current value (capi.cpp)
 int fail(int code, const std::string& m);  // sets the thread-local message, returns code
 int ok();
 int hip_fail(hipError_t e, const char* what);
@@ -45,6 +46,7 @@ struct StreamState {
   uint32_t wf_pool = 0;
   uint32_t* wf_status_host = nullptr;
   uint32_t* wf_status_dev = nullptr;
+  uint64_t wf_iter = 0;  // wavefront iterations launched on this stream so far (status-ring slot numbering)
 };
 
 // Progress of one frame (yart_render's callback): the kernels store `base + units handed out` to
@@ -63,8 +65,8 @@ struct Progress {
 struct yart_scene {
   int device = 0;
   int cu_count = 256;
-  bool wavefront = false;  // mesh scene without EXT features: k_wf_shade / k_wf_trace (YART_MESH_WF=0: megakernel)
-  uint32_t wf_pool = 1u << 20;  // paths in flight (YART_WF_POOL)
+  bool wavefront = false;  // mesh scene without EXT features: k_wf_shade / k_wf_trace (deep meshes, YART_OPT_MESH_WAVEFRONT)
+  uint32_t wf_pool = 1u << 20;  // paths in flight (YART_OPT_WF_POOL)
   yart_dev::DevScene dev{};
   std::vector<void*> owned;
   yart_scene_info info{};

@@ -7,7 +7,6 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -48,13 +47,13 @@ struct WalkBuilder {
   BuiltMesh& m;
   std::vector<WItem> items;
   uint32_t n_tris = 0, max_depth = 10, depth = 0, next_rec = 0;
-  int bins = 32;  // SAH bins per axis (YART_WALK_BINS, A/B)
-  int pick = 0;   // which part the greedy 4-way expansion splits next: 0 area x count, 1 count, 2 area (YART_WALK_PICK)
+  // SAH bins per axis; the greedy 4-way expansion splits the part of largest area x count next
+  // (16 / 32 / 64 bins and count- or area-only picks were within +-2 %)
+  static constexpr int kBins = 32;
 
   // Binned SAH cut of items[b, e) (n >= 2): returns the cut position in (b, e), items partitioned.
   size_t split(size_t b, size_t e) {
-    constexpr int kMaxBins = 128;
-    const int kBins = bins;
+    constexpr int kMaxBins = kBins;
     float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t i = b; i < e; ++i)
       for (int k = 0; k < 3; ++k) { cmin[k] = std::min(cmin[k], items[i].c[k]); cmax[k] = std::max(cmax[k], items[i].c[k]); }
@@ -152,7 +151,7 @@ struct WalkBuilder {
           Box3 pb;
           for (size_t i = parts[k].b; i < parts[k].e; ++i) pb.grow(items[i]);
           const double cnt = (double)(parts[k].e - parts[k].b);
-          const double c = pick == 1 ? cnt : pick == 2 ? pb.area() : pb.area() * cnt;
+          const double c = pb.area() * cnt;
           if (c > most) { most = c; sel = k; }
         }
         const size_t pb = parts[sel].b, pe = parts[sel].e, pc = split(pb, pe);
@@ -185,8 +184,10 @@ void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
   WalkBuilder w{m};
   w.n_tris = (uint32_t)(m.leaves.size() / kTriFloats);
   w.max_depth = max_depth;
-  if (const char* e = std::getenv("YART_WALK_BINS")) w.bins = std::min(128, std::max(2, std::atoi(e)));
-  if (const char* e = std::getenv("YART_WALK_PICK")) w.pick = std::atoi(e);
+  // The walk tree's records follow the n sorted ones, so a leaf's first record index reaches 2n - 1,
+  // and a node id holds it in 27 bits (1<<31 | count<<27 | first): a larger mesh keeps walking the
+  // reference tree front to back (past that bound the index ran into the count bits).
+  if (2ull * w.n_tris > (1ull << 27)) return;
   w.items.resize(w.n_tris);
   for (uint32_t t = 0; t < w.n_tris; ++t) {
     const float* r = &m.leaves[kTriFloats * (size_t)t];

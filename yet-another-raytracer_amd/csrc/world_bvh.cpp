@@ -193,13 +193,7 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     for (int k = 0; k < 3; ++k) items[i].c[k] = 0.5 * (items[i].lo[k] + items[i].hi[k]);
     items[i].idx = (uint32_t)i;
   }
-  // YART_WORLD_SAH=node_cost,max_leaf: tuning sweeps (tools/gpu_world.sh)
-  SahParams prm;
-  if (const char* e = std::getenv("YART_WORLD_SAH")) {
-    double c = 0.0;
-    unsigned l = 0;
-    if (std::sscanf(e, "%lf,%u", &c, &l) == 2 && c > 0.0 && l >= 1) { prm.node_cost = c; prm.max_leaf = l; }
-  }
+  const SahParams prm;  // node cost and leaf size from the r02 sweep (profiles/r02g_world_sah_sweep.txt)
   out.nodes.reserve(2 * objs.size());
   out.nodes.emplace_back();
   build(items, 0, items.size(), 0, 0, out, sah, prm);

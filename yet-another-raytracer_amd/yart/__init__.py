@@ -108,8 +108,48 @@ def load_device():
     _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
     _sig(L, "yart_multi_destroy", None, P)
     _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
+    _sig(L, "yart_debug_set_option", I, I, C.c_int64)
+    _sig(L, "yart_debug_get_option", I, I, C.POINTER(C.c_int64))
     _dev = L
+    # Tools and A/B scripts pass library options as YART_OPTIONS="world_bvh=1,mesh_wavefront=0" to
+    # this glue (tools/ab.py children, bench_configs.py); the library itself reads no environment.
+    for item in filter(None, os.environ.get("YART_OPTIONS", "").split(",")):
+        k, v = item.split("=")
+        set_option(k.strip(), int(v))
     return L
+
+
+# yart_debug_set_option keys (include/yart.h YART_OPT_*)
+OPTIONS = {"qbvh_ties_desc": 0, "qbvh_threads": 1, "walk_tree": 2, "mesh_walk_ref": 3, "world_bvh": 4,
+           "mesh_wavefront": 5, "wf_pool": 6, "scratch_bytes": 7}
+
+
+def get_option(name):
+    v = C.c_int64()
+    _check_dev(load_device().yart_debug_get_option(OPTIONS[name], C.byref(v)))
+    return v.value
+
+
+def set_option(name, value):
+    """Sets a library option (yart_debug_set_option); returns the previous value."""
+    old = get_option(name)
+    _check_dev(load_device().yart_debug_set_option(OPTIONS[name], int(value)))
+    return old
+
+
+class option:
+    """with yart.option("world_bvh", 1): ... — sets a library option and restores it on exit."""
+
+    def __init__(self, name, value):
+        self.name, self.value, self.old = name, value, None
+
+    def __enter__(self):
+        self.old = set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.old)
+        return False
 
 
 def _check_host(rc):
