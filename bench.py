@@ -46,8 +46,21 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
 import yart  # noqa: E402
 from yart.shard import PackedGather  # noqa: E402
+from yart.watchdog import Watchdog, wait_events  # noqa: E402
 
 WORKLOAD = dict(scene="cornell-box", width=800, height=800, spp=256, max_depth=50)
+METRIC = "Msamples/sec (WxHxspp/sec), cornell-box 800x800x256spp depth 50"
+
+# Stage deadlines (yart/watchdog.py): a stage that waits on device work gets 20x
+# the one-GPU frame time per frame it waits for, plus a fixed allowance (120 s; the
+# YART_BENCH_DEADLINE_S environment variable of this script overrides it, for tests), so a hang in a
+# communicator's setup, a render or a gather ends with one JSON line naming the stage and exit 3.
+ONE_GPU_FRAME_S = 0.05  # the C2 frame on one MI355X: 29 ms measured (profiles/r03q_bench_cornell.log), rounded up
+BASE_DEADLINE_S = float(os.environ.get("YART_BENCH_DEADLINE_S", "120"))
+
+
+def frames_deadline(n_frames):
+    return BASE_DEADLINE_S + 20.0 * ONE_GPU_FRAME_S * n_frames
 
 # f64 FLOPs per counted operation (DESIGN.md "Roofline"): add/sub/mul/div/sqrt = 1, compares 0.
 FLOPS = {
@@ -189,13 +202,15 @@ def launch_mode(a):
 def main():
     a = parse()
     mode, world, rank, local = launch_mode(a)
+    wd = Watchdog(METRIC, rank=rank)
     # Rehearsal of the per-rank N>1 path on a 1-GPU box (RCCL refuses two ranks on one device): every
     # rank on device 0, the packed shards gathered over gloo on host copies. Never set for a real run.
     rehearse = mode == "ranks" and os.environ.get("YART_BENCH_SAME_DEVICE") == "1"
     if rehearse:
         local = 0
     if mode == "ranks":
-        dist.init_process_group("gloo")  # control plane only
+        with wd.stage("process group init (gloo control plane)", BASE_DEADLINE_S):
+            dist.init_process_group("gloo")  # control plane only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     W, H, spp, depth = WORKLOAD["width"], WORKLOAD["height"], WORKLOAD["spp"], WORKLOAD["max_depth"]
@@ -204,8 +219,13 @@ def main():
     cam = preset.camera(W, H)
     shard_index, shard_count = (rank, world) if mode == "ranks" else (0, 1)
     prm = yart.render_params(W, H, spp, depth, shard_index=shard_index, shard_count=shard_count, samples_per_unit=a.spu)
-    scene = yart.DeviceScene(preset.desc, device=local)
-    multi = yart.MultiScene(preset, list(range(world))) if mode == "multi" else None
+    with wd.stage(f"scene upload (device {local})", BASE_DEADLINE_S):
+        scene = yart.DeviceScene(preset.desc, device=local)
+    multi = None
+    if mode == "multi":
+        with wd.stage(f"communicator init (yart_multi_create: {world} scene uploads + ncclCommInitAll)",
+                      BASE_DEADLINE_S + 10.0 * world):
+            multi = yart.MultiScene(preset, list(range(world)))
     # Frames alternate over S streams, each with its own frame / packed / RGBA buffers (and, inside
     # libyart, its own sample scratch and unit counter): frame k+1's persistent waves start in the
     # SIMD slots frame k's last long paths leave idle. Every frame is still rendered, gathered and
@@ -232,27 +252,52 @@ def main():
             packed_h, frame_h = torch.zeros_like(packeds[0], device="cpu"), torch.zeros_like(frame, device="cpu")
             gather = PackedGather(W, H, world, rank, torch.device("cpu"))
         else:
-            uid = [yart.Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            ok = 1
-            try:
-                comm = yart.Comm(uid[0], world, rank, local)
-            except yart.YartError as e:
-                print(f"rank {rank}: libyart RCCL communicator failed ({e})", file=sys.stderr, flush=True)
-                ok = 0
-            t = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            if t.item():
-                collective = "ncclGather (libyart yart_gather_frame_async, RCCL, one rank per GPU)"
-            else:  # the same packets through torch's RCCL process group
-                if comm is not None:
-                    comm.close()
-                    comm = None
-                nccl_group = dist.new_group(backend="nccl", device_id=dev)
-                gather = PackedGather(W, H, world, rank, dev)
-                collective = "gather (torch.distributed nccl, fallback)"
+            with wd.stage(f"communicator init (ncclCommInitRank, rank {rank} of {world})", BASE_DEADLINE_S + 10.0 * world):
+                uid = [yart.Comm.unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                ok = 1
+                try:
+                    comm = yart.Comm(uid[0], world, rank, local)
+                except yart.YartError as e:
+                    print(f"rank {rank}: libyart RCCL communicator failed ({e})", file=sys.stderr, flush=True)
+                    ok = 0
+                t = torch.tensor([ok], dtype=torch.int32)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                if t.item():
+                    collective = "ncclGather (libyart yart_gather_frame_async, RCCL, one rank per GPU)"
+                else:  # the same packets through torch's RCCL process group
+                    if comm is not None:
+                        comm.close()
+                        comm = None
+                    nccl_group = dist.new_group(backend="nccl", device_id=dev)
+                    gather = PackedGather(W, H, world, rank, dev)
+                    collective = "gather (torch.distributed nccl, fallback)"
 
     coll_done = [None]  # the previous step's collective (ranks, N > 1): the next one waits for it
+    last = {}           # the latest step's stage events (single / ranks): where a stalled frame stands
+
+    def mark(key, st):
+        ev = torch.cuda.Event()
+        ev.record(st)
+        last[key] = ev
+
+    def where():
+        """The watchdog's diagnosis: the stage the latest frame is stuck in."""
+        if mode == "multi":
+            state, unpacked = multi.query()
+            if min(state) < 0:
+                return {"frame": "being enqueued (a host call into RCCL or the render launch has not returned)"}
+            waiting = [d for d, v in enumerate(state) if v == 0]
+            if waiting:
+                return {"frame": f"render on device(s) {waiting}", "device_state": state}
+            waiting = [d for d, v in enumerate(state) if v == 1]
+            if waiting:
+                return {"frame": f"gather (device(s) {waiting} not through ncclGather)", "device_state": state}
+            return {"frame": "unpack on device 0" if unpacked == 0 else "finalize on device 0", "device_state": state}
+        for key in ("render", "gather", "end"):
+            if key in last and not last[key].query():
+                return {"frame": f"{key} on device {local}" + ("" if key != "gather" else f" (rank {rank} of {world})")}
+        return {"frame": "host side (no device work pending)"}
 
     def step(i, streams=streams):
         k = i % len(streams)
@@ -260,11 +305,13 @@ def main():
         with torch.cuda.stream(st):
             if mode == "single":
                 scene.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
+                mark("render", st)
             elif mode == "multi":
                 multi.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
             else:
                 packed = packeds[k]
                 scene.render_packed_async(cam, prm, packed.data_ptr(), st.cuda_stream)
+                mark("render", st)
                 if coll_done[0] is not None:
                     st.wait_event(coll_done[0])
                 if comm is not None:
@@ -276,14 +323,14 @@ def main():
                         frame.copy_(frame_h)
                 else:
                     gather(packed, frame, dist, group=nccl_group)
-                ev = torch.cuda.Event()
-                ev.record(st)
-                coll_done[0] = ev
+                mark("gather", st)
+                coll_done[0] = last["gather"]
             if rank == 0:
                 rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
                                                  yart.C.c_void_p(rgba.data_ptr()), yart.C.c_void_p(st.cuda_stream))
                 if rc != 0:
                     raise RuntimeError(L.yart_last_error().decode())
+            mark("end", st)
 
     def drain_timing():
         """(render_ms, accumulate_ms or gather_ms, frames) summed over the frames since the last call."""
@@ -296,37 +343,50 @@ def main():
         return r, acc, n
 
     def sync_all():
-        for d in range(world if mode == "multi" else 1):
-            torch.cuda.synchronize(d if mode == "multi" else dev)
+        """Every stream's queued work done, by polling an event on each (in the one-process N-GPU
+        path each frame's unpack waits for every device's render and gather, and the caller stream
+        waits for the unpack, so the caller streams' events cover all devices)."""
+        evs = []
+        for st in streams:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+        wait_events(evs)
 
     # warm-up: W steps, and at least one frame on every stream (its scratch is allocated then)
     prep = max(0, S - a.warmup)
-    for i in range(a.warmup + prep):
-        step(i)
-    sync_all()
+    with wd.stage("warm-up frames", frames_deadline(a.warmup + prep), where):
+        for i in range(a.warmup + prep):
+            step(i)
+        sync_all()
     drain_timing()  # drop the warm-up frames' events
     if mode == "ranks":
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    sync_all()
+        with wd.stage("barrier before the timed frames", BASE_DEADLINE_S):
+            dist.barrier()
+    with wd.stage("timed frames", frames_deadline(a.steps), where):
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(i)
+        sync_all()
     if mode == "ranks":
-        dist.barrier()
+        with wd.stage("barrier after the timed frames", BASE_DEADLINE_S):
+            dist.barrier()
     elapsed = time.perf_counter() - t0
     if mode == "ranks":
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        with wd.stage("max-over-ranks time (all_reduce)", BASE_DEADLINE_S):
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
     render_ms, accum_ms, nfr = drain_timing()
     overlap_ms = render_ms / max(1, nfr)  # k_render launch durations in the timed loop (overlapping for S > 1)
     # The roofline's kernel time: k_render alone. With S > 1 the launches in the timed loop overlap
     # (a launch's events bracket its wait for the slots the previous frame still holds), so the
     # kernel's own duration is taken from 3 frames on one stream right after the timed region.
     if S > 1:
-        for i in range(3):
-            step(i, streams=streams[:1])
-        sync_all()
+        with wd.stage("kernel-time frames (one stream)", frames_deadline(3), where):
+            for i in range(3):
+                step(i, streams=streams[:1])
+            sync_all()
         render_ms, accum_ms, nfr = drain_timing()
     kern_ms = render_ms / max(1, nfr)      # k_render average launch duration (one stream; multi: slowest GPU)
     accum_ms = accum_ms / max(1, nfr)      # k_accumulate (chunked path); multi: the root's gather + unpack
@@ -340,8 +400,9 @@ def main():
         assert torch.isfinite(f).all() and f.abs().sum() > 0
         if world > 1:
             full = torch.zeros_like(frame)
-            scene.render_async(cam, yart.render_params(W, H, spp, depth), full.data_ptr(), stream.cuda_stream)
-            torch.cuda.synchronize(dev)
+            with wd.stage("frame check (one-device render of the whole frame)", frames_deadline(1)):
+                scene.render_async(cam, yart.render_params(W, H, spp, depth), full.data_ptr(), stream.cuda_stream)
+                sync_all()
             assert torch.equal(full, frame), "assembled frame differs from the one-device render"
             frame_check = "assembled frame bitwise equal to the one-device render"
             print(frame_check, file=sys.stderr, flush=True)
@@ -351,7 +412,8 @@ def main():
     cpu = None
     if rank == 0 and not a.no_stats:
         # shard 0's counted work (the whole frame at N = 1) over its kernel time
-        _, st = scene.render_with_stats(cam, yart.render_params(W, H, spp, depth, shard_index=0, shard_count=world))
+        with wd.stage("work counters (instrumented launch)", frames_deadline(10)):
+            _, st = scene.render_with_stats(cam, yart.render_params(W, H, spp, depth, shard_index=0, shard_count=world))
         flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
                  st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
         achieved = flops / (kern_ms * 1e-3) / 1e12
@@ -386,13 +448,14 @@ def main():
         if mode == "multi":
             roofline["gather_ms"] = round(gather_ms, 3)
     if rank == 0 and a.cpu_spp > 0 and world == 1:
-        cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
+        with wd.stage("cpu baseline (oracle on the host cores)", 900.0):
+            cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
 
     if rank == 0:
         samples = W * H * spp
         value = samples * a.steps / elapsed / 1e6
         line = {
-            "metric": "Msamples/sec (WxHxspp/sec), cornell-box 800x800x256spp depth 50",
+            "metric": METRIC,
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference scene preset, seeded Philox RNG)",
@@ -405,12 +468,13 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if comm is not None:
-        comm.close()
-    if multi is not None:
-        multi.close()
-    if mode == "ranks":
-        dist.destroy_process_group()
+    with wd.stage("teardown (communicators, process group)", BASE_DEADLINE_S):
+        if comm is not None:
+            comm.close()
+        if multi is not None:
+            multi.close()
+        if mode == "ranks":
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

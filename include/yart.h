@@ -355,6 +355,11 @@ int yart_render_multi(yart_multi* m, const yart_camera* cam, const yart_render_p
 int yart_multi_frame_timing(yart_multi* m, double* render_ms, double* gather_ms, uint32_t* frames);
 /* Device time of the last yart_render_multi: render (slowest device) and gather + unpack, ms. */
 int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gather_ms);
+/* Where the latest frame submitted to `m` stands, without waiting (a watchdog names the stage a
+ * stalled frame is in): state[d] for each device 0 = rendering, 1 = rendered (its part of the gather
+ * pending), 2 = gathered; *unpacked = 1 once devices[0] has unpacked the frame, else 0. While a
+ * submission is being enqueued (or before the first), every value reads -1. */
+int yart_multi_query(yart_multi* m, int32_t* state, int32_t* unpacked);
 void yart_multi_destroy(yart_multi* m);
 
 /* The root side of the gather on its own (k_unpack_shards): `shards` packets back to back in

@@ -4,6 +4,8 @@ present, `value` is the frame's samples over the step time, `roofline.frac` is a
 `achieved` is the launch's algorithmic FLOPs over the kernel time, and that kernel time agrees
 with rocprofv3's average k_render duration. CPU only: it reads committed files."""
 import csv
+import subprocess
+import sys
 import json
 from pathlib import Path
 
@@ -95,3 +97,38 @@ def test_gpus_flag_never_reports_another_n(args, env):
     assert r.returncode != 0, r.stdout
     assert '"n_gpus"' not in r.stdout
     assert "bench.py: --gpus" in r.stderr
+
+
+def test_watchdog_names_the_stalled_stage_and_exits_3():
+    """yart/watchdog.py: a stage that overruns its deadline prints ONE JSON line naming the stage
+    (and the watchdog's diagnosis of where the frame stands) and ends the process with exit 3."""
+    code = ("import sys, time; sys.path.insert(0, 'yet-another-raytracer_amd');"
+            "from yart.watchdog import Watchdog;"
+            "wd = Watchdog('m', poll_s=0.05);"
+            "ctx = wd.stage('gather', 0.5, lambda: {'frame': 'gather (device(s) [1] not through ncclGather)'});"
+            "ctx.__enter__(); time.sleep(30); print('not reached')")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=str(ROOT))
+    assert r.returncode == 3, (r.returncode, r.stdout, r.stderr)
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in r.stdout
+    e = lines[0]
+    assert e["stage"] == "gather" and "gather" in e["error"] and e["value"] is None
+    assert "device(s) [1]" in e["detail"]["frame"]
+
+
+def test_bench_stalled_first_stage_exits_nonzero_naming_it():
+    """bench.py's N > 1 per-rank path with its peer rank never arriving: the gloo control plane's
+    setup stalls (a real stall, not an injected one), and with a 3 s deadline the run must end with
+    exit 3 and one JSON line whose error names that stage — not a silent kill at the driver's limit.
+    Runs on the CPU: the stage comes before any GPU call."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+           "YART_BENCH_DEADLINE_S": "3"}
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], env)
+    assert r.returncode == 3, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and lines[0]["value"] is None
+    assert lines[0]["stage"].startswith("process group init") and "deadline" in lines[0]["error"]

@@ -601,3 +601,54 @@ def test_errors_are_reported_not_raised(dev):
     with pytest.raises(yart.YartError) as e:
         yart.DeviceScene(b2.desc())
     assert e.value.code == abi.ERR_INVALID
+
+
+def _mesh_triangles(p, k=0):
+    """(n, 3, 3) f64 vertices of mesh k of a preset (the exact f32 values tobj parsed)."""
+    m = p.desc.contents.meshes[k]
+    n = int(m.n_triangles)
+    return np.ctypeslib.as_array(m.positions, shape=(n * 9,)).reshape(n, 3, 3).astype(np.float64)
+
+
+def _near_coplanar_rays(tris, n, seed, reach):
+    """Rays that run within 1e-15 .. 1e-12 rad of a triangle's plane (and some exactly in it, up to
+    rounding) and pass through that triangle's interior, arriving from `reach` units away: the
+    case where Moller-Trumbore's t loses all its digits (condition number 1 / |cos theta|) and the
+    front-to-back walk's pruning margin (2^-8 relative, kernels.hip qbvh_coop) is not a bound."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, len(tris), n)
+    v0, e1, e2 = tris[k, 0], tris[k, 1] - tris[k, 0], tris[k, 2] - tris[k, 0]
+    nrm = np.cross(e1, e2)
+    ln = np.linalg.norm(nrm, axis=1, keepdims=True)
+    ok = ln[:, 0] > 0
+    nrm = np.where(ok[:, None], nrm / np.where(ln > 0, ln, 1.0), np.array([0.0, 1.0, 0.0]))
+    a, b = rng.uniform(0, 1, n), rng.uniform(0, 1, n)
+    f = a + b > 1
+    a[f], b[f] = 1 - a[f], 1 - b[f]
+    X = v0 + a[:, None] * e1 + b[:, None] * e2
+    g = rng.normal(size=(n, 3))
+    u = g - (g * nrm).sum(1, keepdims=True) * nrm
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    tilt = 10.0 ** rng.uniform(-15, -12, n) * rng.choice([-1.0, 1.0], n)
+    tilt[rng.uniform(0, 1, n) < 0.1] = 0.0
+    d = u * np.cos(tilt)[:, None] + nrm * np.sin(tilt)[:, None]
+    d *= 10.0 ** rng.uniform(-1, 1, n)[:, None]  # the renderer's rays are not unit length
+    o = X - rng.uniform(0.05, 1.0, n)[:, None] * reach * d / np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+
+
+@pytest.mark.parametrize("scene,reach", [("david", 120.0), ("sycee", 3.0)])
+def test_mesh_walk_near_coplanar_rays_match_oracle(dev, scene, reach):
+    """200k rays grazing a triangle of the mesh within 1e-15 .. 1e-12 rad of
+    its plane, through its interior, from up to `reach` units away (most of them cross other parts
+    of the mesh first). The front-to-back walk prunes subtrees whose box begins 2^-8 beyond the best
+    hit so far, and Moller-Trumbore's t of a grazed triangle can fall before its own box: the
+    closest hits must still be the reference-order walk's, bitwise (the oracle walks in
+    qbvh.rs:381-543's order with the running t_max)."""
+    p = yart.Preset(scene)
+    rays = _near_coplanar_rays(_mesh_triangles(p), 200000, seed=41, reach=reach)
+    s = yart.DeviceScene(p)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o2 >= 0).mean() > 0.5
+    _hits_equal(h, o, h2, o2)

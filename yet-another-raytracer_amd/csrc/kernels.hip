@@ -727,15 +727,22 @@ __device__ __forceinline__ bool leaf_tri_hit(float4 p0, float4 p1, float4 p2, co
   return !(a > -kEps && a < kEps) && u >= 0.0 && u <= 1.0 && v >= 0.0 && u + v <= 1.0 && t >= tmin && tmax > t;
 }
 
-// Per-lane walk (ConstantMedium boundaries, which hit their mesh from divergent code): one lane,
-// one ray, a 32-slot stack in LDS laid out [slot][lane].
+// Per-lane walk (ConstantMedium boundaries, which hit their mesh from divergent code, and the rare
+// re-walk of the cooperative walk's exact check): one lane, one ray, a 32-slot stack in LDS laid
+// out [slot][lane]. Out of line, with the ray passed and the hit returned by value (in registers):
+// through references, the caller's Ray and hit variables became stack objects, written to scratch
+// at every mesh walk of the world pass whether or not the re-walk ran.
+struct LaneHit { double t, u, v; uint32_t tri, found; };
 template <bool STATS>
-__device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin, double tmax, double& t_hit,
-                                    uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st) {
-  const double ro[3] = {r.o.x, r.o.y, r.o.z}, rd[3] = {r.d.x, r.d.y, r.d.z};
+__device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double ox, double oy, double oz, double dx,
+                                          double dy, double dz, double tmin, double tmax, uint32_t* __restrict__ stk,
+                                          unsigned long long* __restrict__ stv) {
+  const DevMesh& M = *Mp;
+  const double ro[3] = {ox, oy, oz}, rd[3] = {dx, dy, dz};
   const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};
   const uint32_t pos = ray_octant(rd);
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
+  LaneHit hit{0.0, 0.0, 0.0, 0u, 0u};
   bool found = false;
   int cursor = 0;
   stk[0] = M.root;
@@ -744,20 +751,20 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
     if (id >> 31) {
       const uint32_t count = (id >> 27) & 0xFu, first = id & ((1u << 27) - 1u);
       const gfloat4p L = leaves + 3 * (size_t)first;
-      if (STATS) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
+      if (STATS) { stv[ST_LEAVES]++; stv[ST_LEAF_TRIS] += count; }
       for (uint32_t i = 0; i < count; ++i) {  // the running t_max: the first of equal hits stays
         double t, u, v;
         const float4 p2 = ld4(L, 3 * i + 2);
         if (leaf_tri_hit(ld4(L, 3 * i), ld4(L, 3 * i + 1), p2, ro, rd, tmin, tmax, t, u, v)) {
           tmax = t;
-          t_hit = t; u_hit = u; v_hit = v;
-          tri = first + i;
+          hit.t = t; hit.u = u; hit.v = v;
+          hit.tri = first + i;
           found = true;
         }
       }
     } else {
       const gfloat4p N = nodes + 8 * (size_t)id;
-      if (STATS) st.v[ST_NODES]++;
+      if (STATS) stv[ST_NODES]++;
       bool hk[4];
       uint32_t chs[4], rank[4], ordered = 0;  // ordered: bit r = the child of push rank r was hit
 #pragma unroll
@@ -776,7 +783,15 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
     if (cursor == 0) break;
     cursor -= 1;
   }
-  return found;
+  hit.found = found ? 1u : 0u;
+  return hit;
+}
+template <bool STATS>
+__device__ __forceinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin, double tmax, double& t_hit,
+                                       uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st) {
+  const LaneHit h = qbvh_lane<STATS>(&M, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, tmin, tmax, stk, STATS ? st.v : nullptr);
+  if (h.found) { t_hit = h.t; u_hit = h.u; v_hit = h.v; tri = h.tri; }
+  return h.found != 0u;
 }
 
 // Cooperative walk: a quad of lanes (4 consecutive) walks ONE ray, lane k of the quad taking
@@ -812,6 +827,18 @@ __device__ __noinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin,
 // they come from is formed again where it is needed: the exact final check and the reference
 // order. flags: bit 0 front to back allowed, bits 1-3 the ray octant.
 struct CoopRay { double o[3], d[3], tmax; float c32[6], inv32[3]; uint32_t flags; };
+// Once its walk has started, a ray's f32 constants are in its quad's registers and the record's
+// c32 / inv32 words are free: the best hit so far goes there (t, u, v as f64 in c32, the triangle in
+// inv32[0], found in inv32[1]), so o and d stay intact and the post-walk check reads its ray back
+// from LDS instead of the caller keeping it in registers across the walk.
+__device__ __forceinline__ void coop_put_d(float* w, double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  w[0] = __uint_as_float((uint32_t)b);
+  w[1] = __uint_as_float((uint32_t)(b >> 32));
+}
+__device__ __forceinline__ double coop_get_d(const float* w) {
+  return __longlong_as_double((long long)(((uint64_t)__float_as_uint(w[1]) << 32) | __float_as_uint(w[0])));
+}
 typedef uint16_t CoopEnt;  // a stack entry's box entry, the upper half of the f32, rounded down
 constexpr int kCoopRayBytes = 64 * (int)sizeof(CoopRay);
 // Per-quad stack slots (node id + its box entry, CoopEnt): 32 for meshes of depth <= 10 (3 depth + 1
@@ -1006,7 +1033,10 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
   constexpr bool kPostCheck = SLOTS == kCoopSlots;
   // The best hit so far is written to the ray's LDS record by the lane that found it (the
   // record's inputs are in registers from take() on), so the walk keeps only its t in registers.
-  double ro[3], rd[3], tin = 0.0, tb = 0.0, teff = 0.0;
+  // The walked ray (o, d, t_max) stays in its LDS record and is read where the f64 arithmetic
+  // needs it — the leaf test, the exact checks, the reference order — not held in 14 VGPRs
+  // through every round of the walk.
+  double tb = 0.0;
   const float tmin32 = (float)(tmin - fabs(tmin) * 0x1p-20);
   float inv32[3], teff32 = 0.0f;  // front to back: the f32 box test (child_hit_f32)
   vfloat2 c32[3];
@@ -1019,9 +1049,9 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     bkey = 0xFFFFFFFFu;
     cursor = 0;
     fnd = false;
-    tb = tin;    // best so far (reference order: the running t_max)
-    teff = tin;  // the t_max child boxes are tested against
-    teff32 = (float)(tin + fabs(tin) * 0x1p-20);
+    const double tin = rays[ray].tmax;
+    tb = tin;  // best so far (reference order: the running t_max, which child boxes are tested against)
+    teff32 = (float)(tin + fabs(tin) * 0x1p-20);  // front to back: the f32 t_max of the child tests
     bound = INFINITY;
     f2b = front_to_back;
   };
@@ -1029,12 +1059,10 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     const CoopRay& s = rays[ray];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      ro[j] = s.o[j]; rd[j] = s.d[j];
       inv32[j] = s.inv32[j];
       c32[j] = vfloat2{s.c32[2 * j], s.c32[2 * j + 1]};
     }
     const uint32_t fl = s.flags;
-    tin = s.tmax;
     pos = fl >> 1;
     restart((fl & 1u) != 0u);
   };
@@ -1077,7 +1105,9 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
           double tt, uu, vv;
           // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
           // back: the tie goes to the reference's visiting order)
-          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, tin, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
+          const CoopRay& s = rays[ray];
+          const double ro[3] = {s.o[0], s.o[1], s.o[2]}, rd[3] = {s.d[0], s.d[1], s.d[2]};
+          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, s.tmax, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
             t = tt; u = uu; v = vv;
             id = __float_as_uint(p2.w);  // sorted index: the normal table's row
             key = f2b ? (aux[li].rank[pos] << 4) | (__float_as_uint(p2.z) << 2) | c : c;
@@ -1095,16 +1125,15 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
             tb = t; fnd = true; bleaf = li; bkey = key;
             if (c == w) {
               CoopRay& s = rays[ray];
-              s.o[0] = t; s.o[1] = u; s.o[2] = v;
-              s.d[0] = __longlong_as_double((long long)((1ull << 32) | id));
+              coop_put_d(&s.c32[0], t); coop_put_d(&s.c32[2], u); coop_put_d(&s.c32[4], v);
+              s.inv32[0] = __uint_as_float(id);
+              s.inv32[1] = __uint_as_float(1u);
             }
             if (f2b) {
-              const double lim = t * (1.0 + kF2bMargin);
-              teff = lim < tin ? lim : tin;
+              const double lim = t * (1.0 + kF2bMargin), tin = rays[ray].tmax;
+              const double teff = lim < tin ? lim : tin;
               teff32 = (float)(teff + teff * 0x1p-20);
               bound = (float)lim;
-            } else {
-              teff = t;
             }
           }
         }
@@ -1123,8 +1152,10 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
           ent = fminf(ent, 3.0e38f);
         } else {
           double l;
-          const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};  // the reference order (rare)
-          hk = child_hit_l(lo, hi, ro, inv, tmin, teff, l);
+          const CoopRay& s = rays[ray];  // the reference order (rare): t_max is the best so far
+          const double ro[3] = {s.o[0], s.o[1], s.o[2]};
+          const double inv[3] = {1.0 / s.d[0], 1.0 / s.d[1], 1.0 / s.d[2]};
+          hk = child_hit_l(lo, hi, ro, inv, tmin, tb, l);
           ent = 0.0f;  // unused in the reference order
         }
         // push rank: reference order from ORDER_TABLE (precomputed per octant); front to back
@@ -1179,11 +1210,12 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
         // W is the reference's answer if its leaf box passes the reference's f64 test at t_max_in
         // (the f32 test visits a superset) and W's t is not before that box's entry (above)
         const auto& A = aux[bleaf];
-        double l = tmin, h = tin;
+        const CoopRay& s = rays[ray];
+        double l = tmin, h = s.tmax;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const double iv = 1.0 / rd[j];  // as formed at staging: the reference's slab test
-          const double t0 = ((double)A.lo[j] - ro[j]) * iv, t1 = ((double)A.hi[j] - ro[j]) * iv;
+          const double iv = 1.0 / s.d[j];  // as formed at staging: the reference's slab test
+          const double t0 = ((double)A.lo[j] - s.o[j]) * iv, t1 = ((double)A.hi[j] - s.o[j]) * iv;
           l = fmax(l, fmin(t0, t1));
           h = fmin(h, fmax(t0, t1));
         }
@@ -1194,7 +1226,7 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
         }
       }
     }
-    if (fin && !fnd && c == 0) rays[ray].d[0] = 0.0;  // no hit (a hit's record is already written)
+    if (fin && !fnd && c == 0) rays[ray].inv32[1] = 0.0f;  // no hit (a hit's record is already written)
     const uint64_t fm = __ballot(fin && c == 0);
     if (fm) {
       if (fin) {
@@ -1211,21 +1243,24 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
   // ray that fails walks again in the reference's order, per lane (qbvh_t, a 32-slot stack in this
   // wave's LDS, free once every lane has read its record) — rare.
   bool redo = false;
+  Ray wr;  // the walked ray, read back from its record (the caller's copy need not live through the walk)
   if (walk) {
     const CoopRay& s = rays[rank];
-    const uint64_t res = (uint64_t)__double_as_longlong(s.d[0]);
-    found = (res >> 32) != 0;
-    t_hit = s.o[0]; u_hit = s.o[1]; v_hit = s.o[2];
-    tri = (uint32_t)res;
+    found = __float_as_uint(s.inv32[1]) != 0u;
+    t_hit = coop_get_d(&s.c32[0]); u_hit = coop_get_d(&s.c32[2]); v_hit = coop_get_d(&s.c32[4]);
+    tri = __float_as_uint(s.inv32[0]);
     const uint32_t fl = s.flags;
-    if (kPostCheck && (fl >> 31))
-      redo = !coop_check(aux, fl & 0x3FFFFFFFu, r, tmin, tmax_in, t_hit) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+    if (kPostCheck && (fl >> 31)) {
+      wr.o = mk(s.o[0], s.o[1], s.o[2]);
+      wr.d = mk(s.d[0], s.d[1], s.d[2]);
+      redo = !coop_check(aux, fl & 0x3FFFFFFFu, wr, tmin, tmax_in, t_hit) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+    }
   }
   if (kPostCheck && __ballot(redo) != 0ull) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (redo) {
       if (STATS) st.v[ST_REWALK]++;
-      found = qbvh_t<STATS>(M, r, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
+      found = qbvh_t<STATS>(M, wr, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
     }
   }
 }
@@ -1837,7 +1872,10 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
                                            double hu, double hv, int wbin, const Ray& ray, double T, uint32_t depth,
                                            Stats& st, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_,
                                            bool& term_) {
-  T_ = T; o_ = ray.o; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false;
+  // o_ starts at the hit point, not the incoming ray's origin: only an ended path keeps the initial
+  // value, and nothing reads its ray again; the origin then dies with the world pass that used it
+  // instead of living (spilled) around the loop to here.
+  T_ = T; o_ = hp; d_ = ray.d; depth_ = depth; R_ = 0.0; term_ = false;
   const DevMaterial& m = S.materials[hmat];
   const uint32_t kind = m.kind;
   if (kind == YART_MAT_LAMBERTIAN) {  // material.rs:44-61, main.rs:556-581
@@ -2053,7 +2091,8 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
     }
     const bool run = DYN ? !need : alive;  // DYN: a lane still asking has found the queue drained
     if (__ballot(run) == 0) break;
-    double R = 0.0;
+    // T is the path's throughput while it runs and its result R (ray_reflectance's return value)
+    // once it has ended (term): one register pair for both, since no lane needs both at once.
     bool term = false, want = false;
     if (run) {
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
@@ -2091,11 +2130,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
           Ieee im;
           scatter(im, nT, no, nd, ndepth, nR, nterm);
         }
-        T = nT; ray.o = no; ray.d = nd; depth = ndepth; R = nR; term = nterm;
+        T = nterm ? nR : nT; ray.o = no; ray.d = nd; depth = ndepth; term = nterm;
       }
       if (!term) {
         if (depth == 0) {  // main.rs:544-546: exhausted depth reflects 1.0
-          R = T * 1.0;
+          T = T * 1.0;
           term = true;
         } else {
           want = true;
@@ -2116,7 +2155,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
       if (want && !term) {
         if (STATS) st.v[ST_SEGMENTS]++;
         if (!hit) {
-          R = T * S.background[wbin];  // background_color.reflect (main.rs:587)
+          T = T * S.background[wbin];  // background_color.reflect (main.rs:587)
           term = true;
         } else {
           const DevMaterial& m = S.materials[h.mat];
@@ -2127,7 +2166,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
           } else {  // DiffuseLight emits on its front face; NoMaterial emits 0 (material.rs:347-355)
             double emitted = 0.0;
             if (kind == YART_MAT_DIFFUSE_LIGHT && h.ff) emitted = texture_value<EXT>(S, m.texture, wbin, h.p, h.u, h.v);
-            R = T * emitted;
+            T = T * emitted;
             term = true;
           }
         }
@@ -2141,6 +2180,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
       if (EXT) { hu = scat ? h.u : 0.0; hv = scat ? h.v : 0.0; }
     }
     if (run && term) {  // ray_color + sanitize_sample_xyz + += (main.rs:526-535, 448-459, 700-707)
+      const double R = T;
       double cx, cy, cz;
       cie_xyz(ray.wl, cx, cy, cz);
       double sx = cx * R, sy = cy * R, sz = cz * R;

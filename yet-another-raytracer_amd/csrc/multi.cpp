@@ -142,6 +142,7 @@ struct MultiSlot {
   std::vector<double*> packed;        // per device, packet_len doubles
   std::vector<size_t> packed_bytes;
   std::vector<hipEvent_t> gathered;   // per device: its ncclGather of the latest frame
+  std::vector<hipEvent_t> rendered;   // per device: its render of the latest frame (yart_multi_query)
   hipEvent_t start = nullptr;         // devices[0]: the caller stream's work before the frame
   hipEvent_t done = nullptr;          // devices[0]: the frame unpacked
   double* recv = nullptr;             // devices[0]: every shard's packet
@@ -159,6 +160,7 @@ struct yart_multi {
   std::mutex mu;                                   // submissions are enqueued one at a time
   std::map<hipStream_t, std::unique_ptr<MultiSlot>> slots;  // by caller stream (devices[0]), at most kMaxSlots
   uint64_t submissions = 0;
+  MultiSlot* latest = nullptr;  // the slot of the latest submission (yart_multi_query)
   std::vector<hipEvent_t> last_gather;             // per device: the latest submission's gather
   hipStream_t host_stream = nullptr;               // devices[0]: yart_render_multi's caller stream
   double* frame = nullptr;                         // devices[0]: yart_render_multi's frame
@@ -177,6 +179,7 @@ struct yart_multi {
       (void)hipSetDevice(devices[(size_t)d]);
       if ((size_t)d < s.packed.size() && s.packed[(size_t)d]) (void)hipFree(s.packed[(size_t)d]);
       if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
+      if ((size_t)d < s.rendered.size() && s.rendered[(size_t)d]) (void)hipEventDestroy(s.rendered[(size_t)d]);
       if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamDestroy(s.streams[(size_t)d]);
       if (d == 0) {
         for (auto& e : s.gather_events) gather_pool.push_back(e);  // unread timings are dropped
@@ -220,6 +223,7 @@ int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
     auto lru = m->slots.begin();
     for (auto it = m->slots.begin(); it != m->slots.end(); ++it)
       if (it->second->last_use < lru->second->last_use) lru = it;
+    if (m->latest == lru->second.get()) m->latest = nullptr;
     m->release_slot(*lru->second);
     m->slots.erase(lru);
   }
@@ -230,10 +234,12 @@ int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
     s->packed.assign((size_t)m->n, nullptr);
     s->packed_bytes.assign((size_t)m->n, 0);
     s->gathered.assign((size_t)m->n, nullptr);
+    s->rendered.assign((size_t)m->n, nullptr);
     for (int d = 0; d < m->n; ++d) {
       HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
       HIP_TRY(hipStreamCreateWithFlags(&s->streams[(size_t)d], hipStreamNonBlocking), "hipStreamCreate");
       HIP_TRY(hipEventCreateWithFlags(&s->gathered[(size_t)d], hipEventDisableTiming), "hipEventCreate");
+      HIP_TRY(hipEventCreateWithFlags(&s->rendered[(size_t)d], hipEventDisableTiming), "hipEventCreate");
       if (d == 0) {
         HIP_TRY(hipEventCreateWithFlags(&s->start, hipEventDisableTiming), "hipEventCreate");
         HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming), "hipEventCreate");
@@ -297,7 +303,9 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
     if (int rc = make_args(m->scenes[di], cam, &q, S->packed[di], a)) return rc;
     a.packed = 1;
     Progress* pr = prog ? &(*prog)[di] : nullptr;
-    return launch_frame(m->scenes[di], a, p->samples_per_unit, false, st, pr);
+    if (int rc = launch_frame(m->scenes[di], a, p->samples_per_unit, false, st, pr)) return rc;
+    HIP_TRY(hipEventRecord(S->rendered[di], st), "hipEventRecord");
+    return YART_OK;
   };
   if (n > 1 && m->scenes[0]->wavefront) {
     std::vector<int> rcs((size_t)n, YART_OK);
@@ -366,6 +374,7 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   HIP_TRY(hipEventRecord(gev.second, S->streams[0]), "hipEventRecord");
   HIP_TRY(hipEventRecord(S->done, S->streams[0]), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(caller, S->done, 0), "hipStreamWaitEvent");
+  m->latest = S;
   return YART_OK;
 }
 
@@ -507,6 +516,26 @@ int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gathe
   if (!m || !render_ms || !gather_ms) return fail(YART_ERR_INVALID, "null argument");
   *render_ms = m->render_ms;
   *gather_ms = m->gather_ms;
+  return ok();
+}
+
+int yart_multi_query(yart_multi* m, int32_t* state, int32_t* unpacked) {
+  if (!m || !state || !unpacked) return fail(YART_ERR_INVALID, "null argument");
+  // never waits: a submission in progress (its thread may be blocked in the gather's setup) holds the
+  // lock, and then every device reads -1
+  std::unique_lock<std::mutex> lk(m->mu, std::try_to_lock);
+  *unpacked = -1;
+  for (int d = 0; d < m->n; ++d) state[d] = -1;
+  if (!lk.owns_lock() || !m->latest) return ok();
+  RestoreDevice restore;
+  MultiSlot& S = *m->latest;
+  auto done = [](hipEvent_t e) { return e && hipEventQuery(e) == hipSuccess; };
+  for (int d = 0; d < m->n; ++d) {
+    (void)hipSetDevice(m->devices[(size_t)d]);
+    state[d] = done(S.gathered[(size_t)d]) ? 2 : done(S.rendered[(size_t)d]) ? 1 : 0;
+  }
+  (void)hipSetDevice(m->devices[0]);
+  *unpacked = done(S.done) ? 1 : 0;
   return ok();
 }
 

@@ -107,6 +107,8 @@ def load_device():
     _sig(L, "yart_unpack_shards_async", I, I, P, U32, U64, U32, U32, P, P)
     _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
     _sig(L, "yart_multi_destroy", None, P)
+    if hasattr(L, "yart_multi_query"):  # diagnostics only (bench.py's watchdog); absent from older A/B builds
+        _sig(L, "yart_multi_query", I, P, P, P)
     _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
     _sig(L, "yart_debug_set_option", I, I, C.c_int64)
     _sig(L, "yart_debug_get_option", I, I, C.POINTER(C.c_int64))
@@ -396,6 +398,14 @@ class MultiScene:
         r, g, n = C.c_double(), C.c_double(), C.c_uint32()
         _check_dev(load_device().yart_multi_frame_timing(self._m, C.byref(r), C.byref(g), C.byref(n)))
         return r.value, g.value, n.value
+
+    def query(self):
+        """yart_multi_query: (per-device state of the latest frame: 0 rendering, 1 rendered,
+        2 gathered, -1 unknown; unpacked 1 / 0 / -1). Never waits."""
+        st = (C.c_int32 * len(self.devices))()
+        up = C.c_int32()
+        _check_dev(load_device().yart_multi_query(self._m, st, C.byref(up)))
+        return list(st), up.value
 
     def last_timing(self):
         r, g = C.c_double(), C.c_double()

@@ -117,6 +117,7 @@ DEVICE_SYMBOLS = [
     "yart_debug_force_rewalk",
     "yart_debug_set_option",
     "yart_debug_get_option",
+    "yart_multi_query",
     "yart_shard_packed_len", "yart_render_packed_async", "yart_comm_unique_id", "yart_comm_init_rank",
     "yart_comm_init_all", "yart_comm_destroy", "yart_gather_frame_async", "yart_multi_create", "yart_render_multi",
     "yart_multi_last_timing", "yart_multi_destroy", "yart_qbvh_build", "yart_render_multi_async",
