@@ -208,8 +208,8 @@ typedef struct yart_scene_info {
   uint32_t bvh_max_depth; /* deepest root-to-leaf path in inner nodes                   */
   uint32_t bvh_max_stack; /* traversal stack slots the deepest path can need            */
   uint64_t device_bytes;  /* HBM held by the scene                                      */
-  uint32_t world_nodes;   /* world BVH nodes over the object list (0 = linear walk)     */
-  uint32_t world_depth;   /* its deepest root-to-leaf path                              */
+  uint32_t world_nodes;   /* 4-wide world BVH nodes over the object list (0 = linear walk) */
+  uint32_t world_depth;   /* its deepest root-to-leaf path (4-wide levels)              */
   uint32_t bvh_tied_cuts; /* QBVH median cuts inside a run of equal centroid keys:
                              where Rust's unstable sort (qbvh.rs:679-685) may order differently */
   uint32_t bvh_tied_leaves; /* leaves whose triangle order rests on equal keys              */

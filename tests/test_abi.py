@@ -37,6 +37,16 @@ def test_host_library_exports_every_declared_symbol(repo):
     assert not missing, missing
 
 
+def test_library_reads_no_environment(repo):
+    """behaviour is set through yart_debug_set_option, never the environment."""
+    for name in ("libyart.so", "libyart_host.so"):
+        so = repo / "yet-another-raytracer_amd" / "lib" / name
+        out = subprocess.run(["nm", "-D", "--undefined-only", str(so)], capture_output=True, text=True,
+                             check=True).stdout
+        imported = {line.split()[-1].split("@")[0] for line in out.splitlines() if line.strip()}
+        assert not imported & {"getenv", "secure_getenv", "__secure_getenv"}, name
+
+
 def test_device_library_loads_without_gpu():
     L = yart.load_device()  # loading must not touch the GPU
     assert L.yart_version().decode().startswith("yart-mi355x")

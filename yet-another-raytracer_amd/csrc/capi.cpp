@@ -126,6 +126,7 @@ DevObject to_dev(const yart_object& o) {
     }
   }
   for (int k = 0; k < 24; ++k) d.p[k] = o.p[k];
+  for (uint32_t l = 0; l < d.n_xf && l < (uint32_t)kMaxXforms; ++l) d.rotated |= d.xf_kind[l] == YART_XF_ROTATE_Y;
   return d;
 }
 
@@ -195,6 +196,7 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
         d->textures[m.texture].kind == YART_TEX_IMAGE)
       return fail(YART_ERR_UNSUPPORTED, "ImageTexture on a mesh (its texcoords are not uploaded)");
   }
+  if (d->n_objects >= kMaxListObjects) return fail(YART_ERR_UNSUPPORTED, "more than 2^29 - 1 world objects");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
   if (device < 0 || device >= ndev) return fail(YART_ERR_INVALID, "device index out of range");
@@ -325,15 +327,23 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   }
   HIP_TRY(upload(s->owned, dm.data(), dm.size(), &ds.meshes, bytes), "upload meshes");
   if (use_world) {
-    HIP_TRY(upload(s->owned, world.nodes.data(), world.nodes.size(), &ds.world_nodes, bytes), "upload world nodes");
+    HIP_TRY(upload(s->owned, world.nodes4.data(), world.nodes4.size(), &ds.world_nodes, bytes), "upload world nodes");
     HIP_TRY(upload(s->owned, world.objs.data(), world.objs.size(), &ds.world_objs, bytes), "upload world objects");
     HIP_TRY(upload(s->owned, world.sph.data(), world.sph.size(), &ds.world_sph, bytes), "upload world spheres");
-    ds.n_world_nodes = (uint32_t)world.nodes.size();
+    ds.n_world_nodes = (uint32_t)world.nodes4.size();
   }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
   ds.has_mesh = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
+  // the shared-reciprocal rect divides (kernels.hip AxisRcp) need every rect / box coordinate (and
+  // so every numerator k - o) within 2^299
+  ds.rcp_ok = 1;
+  for (uint32_t i = 0; i < d->n_objects; ++i) {
+    const yart_object& o = d->objects[i];
+    if (o.kind >= YART_PRIM_XY_RECT && o.kind <= YART_PRIM_BOX)
+      for (int k = 0; k < (o.kind == YART_PRIM_BOX ? 6 : 5); ++k) ds.rcp_ok &= std::fabs(o.p[k]) <= 0x1p299 ? 1u : 0u;
+  }
   ds.has_ext = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_ext |= d->objects[i].n_xforms && d->objects[i].xforms[0].kind == YART_XF_MEDIUM;
   for (uint32_t i = 0; i < d->n_materials; ++i) ds.has_ext |= d->materials[i].kind == YART_MAT_ISOTROPIC;
@@ -365,8 +375,8 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   in.bvh_nodes = nodes; in.bvh_leaves = leaves; in.bvh_max_depth = depth;
   in.bvh_max_stack = d->n_meshes ? 3 * depth + 1 : 0;
   in.device_bytes = bytes;
-  in.world_nodes = use_world ? (uint32_t)world.nodes.size() : 0;
-  in.world_depth = use_world ? world.depth : 0;
+  in.world_nodes = use_world ? (uint32_t)world.nodes4.size() : 0;
+  in.world_depth = use_world ? world.depth4 : 0;
   in.bvh_tied_cuts = tied_cuts;
   in.bvh_tied_leaves = tied_leaves;
   in.bvh_build_ms = build_ms;

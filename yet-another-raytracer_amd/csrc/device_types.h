@@ -1,7 +1,7 @@
 // device_types.h — HBM layout of a scene on one MI355X (shared by the host side of libyart and
 // the kernels). Everything the per-sample loop reads is resident; nothing is rebuilt per frame.
 //
-//  DevObject   world / light list entries in list order (hittable.rs:47-123). 320 B each; a wave
+//  DevObject   world / light list entries in list order (hittable.rs:47-123). 328 B each; a wave
 //              walks the list with a wave-uniform index, so the fields come in on the scalar path.
 //  DevMaterial material table (material.rs), 64 B.
 //  DevTexture  36-bin spectra precomputed from RGB with the Smits basis (color.rs:54-90): the
@@ -23,6 +23,7 @@ namespace yart_dev {
 constexpr int kMaxXforms = 4;
 constexpr int kBins = 36;
 constexpr int kStackSlots = 32;     // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
+constexpr uint32_t kMaxListObjects = 1u << 29;  // the world pass keeps obj << 3 | sub in one word (kernels.hip HitId)
 constexpr int kMaxStackSlots = 64;  // the reference's stack (qbvh.rs:382-384): depth <= 21 (wavefront path)
 
 struct DevObject {
@@ -30,6 +31,8 @@ struct DevObject {
   uint32_t xf_kind[kMaxXforms];
   double xf[kMaxXforms][3];  // TRANSLATE: offset; ROTATE_Y: sin, cos (hittable.rs:173-176)
   double p[24];
+  uint32_t rotated;  // a RotateY wrapper turns the ray's direction (the shared reciprocals do not apply)
+  uint32_t pad_;
 };
 
 struct DevMaterial {
@@ -115,6 +118,19 @@ constexpr uint32_t kWorldLeafSpheres = 1u;  // every object of the leaf is a sph
 constexpr uint32_t kWorldHandleMaxCount = 15u;
 constexpr uint32_t kWorldHandleFirstMask = 1u << 27;
 static_assert(sizeof(DevWorldNode) == 48, "DevWorldNode must be 48 B");
+// The 4-wide world BVH the device walks (the binary tree above collapsed, two levels per node: each
+// node's four children are the binary tree's nodes two levels down, or fewer where leaves come
+// earlier): per child its f32 box (rounded outward as above), magnitude (margin scale) and handle,
+// laid out per axis so one lane reads a whole node with eight 16-B loads. An empty child slot has
+// the handle kWorld4Empty and is never tested.
+struct alignas(16) DevWorldNode4 {
+  float bmin[3][4];   // [axis][child]
+  float bmax[3][4];
+  float mag[4];
+  uint32_t handle[4]; // a node handle as above: leaf count << 28 | sphere flag | first slot, or an inner node's index
+};
+static_assert(sizeof(DevWorldNode4) == 128, "DevWorldNode4 must be 128 B");
+constexpr uint32_t kWorld4Empty = 0xFFFFFFFFu;
 
 struct DevScene {
   const DevObject* objects;
@@ -123,7 +139,7 @@ struct DevScene {
   const DevTexture* textures;
   const DevMesh* meshes;
   const double* background;  // 36 bins
-  const DevWorldNode* world_nodes;  // null: walk the list linearly
+  const DevWorldNode4* world_nodes;  // the 4-wide world BVH (root = node 0); null: walk the list linearly
   const uint32_t* world_objs;
   const double* world_sph;   // per world_objs slot: centre xyz, radius (plain spheres; else 0)
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
@@ -132,6 +148,7 @@ struct DevScene {
   uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
   uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
+  uint32_t rcp_ok;   // every rect / box coordinate within 2^299: the shared-reciprocal divides apply (kernels.hip AxisRcp)
 };
 
 }  // namespace yart_dev

@@ -551,13 +551,49 @@ __device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r,
   h.t = t; h.p = pt;
 }
 
-// aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
-template <int A, int B, int CC>
-__device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
+// Shared reciprocals of a ray's direction for the rect and box-face tests of one world pass: the
+// rects of one axis divide by the same d[A], and the IEEE quotient's first half (scale, v_rcp_f64,
+// two Newton steps) depends on the denominator only. With r = rcp_core(d[A]), the quotient is
+// q = RN(n r) corrected once by its exact fma residual (Markstein): bitwise RN(n / d[A]) for any
+// sign when |d[A]| is in [2^-300, 2^300] and |n| <= 2^300 (no scaling, overflow or underflow in the
+// steps). A quotient with |n| < 2^-600 may differ, but both are then below 2^-299, under t_min.
+// `ok` holds those ranges for the ray (|o| <= 2^299, and capi.cpp checks |k| <= 2^299 for every
+// rect and box coordinate of the scene, DevScene::rcp_ok) and t_min >= 2^-299; a lane without it
+// divides on the IEEE sequence (a rarely taken branch).
+struct AxisRcp { double r[3]; bool ok; };
+__device__ __forceinline__ AxisRcp axis_rcp(const Ray& ray, double tmin, bool scene_ok) {
+  AxisRcp q;
+  const double* o = &ray.o.x;
+  const double* d = &ray.d.x;
+  bool ok = scene_ok && tmin >= 0x1p-299;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    ok = ok && fabs(d[j]) >= 0x1p-300 && fabs(d[j]) <= 0x1p300 && fabs(o[j]) <= 0x1p299;
+    q.r[j] = rcp_core(d[j]);
+  }
+  q.ok = ok;
+  return q;
+}
+__device__ __forceinline__ double quo_rcp(double n, double d, double r) {  // RN(n / d) in AxisRcp's ranges
+  const double q = n * r;
+  const double remn = __builtin_fma(d, q, -n);
+  return __builtin_fma(-remn, r, q);
+}
+
+// aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k. RCP: t from the ray's shared
+// reciprocal (rc, above).
+template <int A, int B, int CC, bool RCP = false>
+__device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t,
+                                       const AxisRcp* rc = nullptr) {
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
-  t = num / den;
+  if (RCP) {
+    t = quo_rcp(num, den, rc->r[A]);
+    if (!rc->ok) t = num / den;
+  } else {
+    t = num / den;
+  }
   if (t < tmin || t > tmax) return false;
   double x = o[B] + t * d[B];
   double y = o[CC] + t * d[CC];
@@ -622,20 +658,25 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
 
 // BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
 // 4-5 yz, so the face's plane axis is 2 - face / 2.
-__device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face) {
+// RCP: the six faces divide by the box's (local) ray's shared reciprocals, formed here once.
+template <bool RCP = false>
+__device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face,
+                                      bool scene_ok = false) {
   if (!box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
   double closest = tmax, tt;
   double s[5];
+  AxisRcp rc;
+  if (RCP) rc = axis_rcp(r, tmin, scene_ok);
   s[0] = p[0]; s[1] = p[3]; s[2] = p[1]; s[3] = p[4];
-  s[4] = p[2]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 0; found = true; }
-  s[4] = p[5]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 1; found = true; }
+  s[4] = p[2]; if (rect_t<2, 0, 1, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 0; found = true; }
+  s[4] = p[5]; if (rect_t<2, 0, 1, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 1; found = true; }
   s[2] = p[2]; s[3] = p[5];
-  s[4] = p[1]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 2; found = true; }
-  s[4] = p[4]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 3; found = true; }
+  s[4] = p[1]; if (rect_t<1, 0, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 2; found = true; }
+  s[4] = p[4]; if (rect_t<1, 0, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 3; found = true; }
   s[0] = p[1]; s[1] = p[4];
-  s[4] = p[0]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 4; found = true; }
-  s[4] = p[3]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 5; found = true; }
+  s[4] = p[0]; if (rect_t<0, 1, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 4; found = true; }
+  s[4] = p[3]; if (rect_t<0, 1, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 5; found = true; }
   t = closest;
   return found;
 }
@@ -657,6 +698,19 @@ __device__ __forceinline__ bool triangle_t(const double* p, const Ray& r, double
   t = f * dot(e2, q);
   if (t < tmin || t > tmax) return false;
   return true;
+}
+// triangle_t's u and v for a triangle it accepted (the same expressions on the same inputs): the
+// world pass keeps only t and who won, and the winner's record recomputes these.
+__device__ __forceinline__ void triangle_uv(const double* p, const Ray& r, double& u, double& v) {
+  V3 v0 = ld3(p), v1 = ld3(p + 3), v2 = ld3(p + 6);
+  V3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+  V3 hh = cross(r.d, e2);
+  double a = dot(e1, hh);
+  double f = 1.0 / a;
+  V3 s = sub(r.o, v0);
+  u = f * dot(s, hh);
+  V3 q = cross(s, e1);
+  v = f * dot(r.d, q);
 }
 template <bool UV = false>
 __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, double t, double u, double v, Hit& h) {
@@ -938,7 +992,10 @@ __device__ __forceinline__ void walk_fault(unsigned int bit) { atomicOr(&g_walk_
 struct CoopStage { float inv32[3], c32[6]; uint32_t flags; bool walk; };
 __device__ __forceinline__ CoopStage coop_stage(const DevMesh& M, bool has_aux, const Ray& r, float tmin32, double tmax) {
   CoopStage s;
-  const double so[3] = {r.o.x, r.o.y, r.o.z}, sdir[3] = {r.d.x, r.d.y, r.d.z};
+  double so[3] = {r.o.x, r.o.y, r.o.z}, sdir[3] = {r.d.x, r.d.y, r.d.z};
+  // Opaque here: hoisted out of the world pass's object loop, these constants were spilled at
+  // every segment and reloaded at every mesh (5 stack slots); recomputed here they cost a few VALU.
+  asm volatile("" : "+v"(sdir[0]), "+v"(sdir[1]), "+v"(sdir[2]));
   const float extent = M.extent;
   double iv[3];
   bool ok = has_aux && extent < 1e15f;
@@ -1087,11 +1144,14 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
 #ifdef YART_WALK_CHECK
         if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
 #endif
-        double t = INFINITY, u = 0.0, v = 0.0;
         // A candidate's key orders equal t's as the reference visits them: front to back (either
         // tree) by (the reference leaf's depth-first rank for this octant, lane in that leaf) and
         // the quad lane in the low bits; in the reference's own order the lower lane of the leaf.
-        uint32_t key = 0xFFFFFFFFu, id = 0u, li = 0u;
+        // t and key take their no-candidate values in one select after the test: set up front,
+        // the defaults were copied again at every exit of the short-circuited test.
+        double tt, u, v;
+        uint32_t kk, id, li;
+        bool cand = false;
         if (c < count) {
           const gfloat4p R = leaves + 3 * (size_t)(first + c);
           float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
@@ -1102,17 +1162,18 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
 #ifdef YART_WALK_CHECK
           if (li >= M.n_leaves) { walk_fault(2u); li = 0u; }
 #endif
-          double tt, uu, vv;
           // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
           // back: the tie goes to the reference's visiting order)
           const CoopRay& s = rays[ray];
           const double ro[3] = {s.o[0], s.o[1], s.o[2]}, rd[3] = {s.d[0], s.d[1], s.d[2]};
-          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, s.tmax, tt, uu, vv) && (tt < tb || (f2b && tt == tb))) {
-            t = tt; u = uu; v = vv;
+          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, s.tmax, tt, u, v) && (tt < tb || (f2b && tt == tb))) {
+            cand = true;
             id = __float_as_uint(p2.w);  // sorted index: the normal table's row
-            key = f2b ? (aux[li].rank[pos] << 4) | (__float_as_uint(p2.z) << 2) | c : c;
+            kk = f2b ? (aux[li].rank[pos] << 4) | (__float_as_uint(p2.z) << 2) | c : c;
           }
         }
+        double t = cand ? tt : INFINITY;
+        uint32_t key = cand ? kk : 0xFFFFFFFFu;
         if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
         quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
         quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
@@ -1293,18 +1354,24 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 
 // ------------------------------------------------------------------------ world hit
 // Which primitive of the world list won, and where: enough to rebuild its record exactly.
+// Which primitive of the world list won, and where: enough to rebuild its record exactly. In the
+// list and world-BVH kernels the world pass keeps t and one word, obj << 3 | sub (sub = a box face;
+// every update is then one 64-bit and one 32-bit select), and the record recomputes a triangle's
+// u, v; the mesh kernels carry u, v and the triangle (a mesh hit's walk result) through the pass.
 struct HitId { double t, u, v; uint32_t obj, sub; };
 
-template <bool HAS_MESH, bool STATS>
+// RCP: rects divide by the shared reciprocals `rc` of the ray they are given (the caller's
+// world-pass reciprocals, or the object's own when a RotateY changed the direction).
+template <bool HAS_MESH, bool STATS, bool RCP = false>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
                                        double tmin, double tmax, double& t, uint32_t& sub, double& u, double& v,
-                                       uint32_t* stk, Stats& st) {
+                                       uint32_t* stk, Stats& st, const AxisRcp* rc = nullptr) {
   switch (kind) {
     case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_t(o.p, r, tmin, tmax, t);
-    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1>(o.p, r, tmin, tmax, t);
-    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2>(o.p, r, tmin, tmax, t);
-    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2>(o.p, r, tmin, tmax, t);
-    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t(o.p, r, tmin, tmax, t, sub);
+    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1, RCP>(o.p, r, tmin, tmax, t, rc);
+    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2, RCP>(o.p, r, tmin, tmax, t, rc);
+    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2, RCP>(o.p, r, tmin, tmax, t, rc);
+    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t<RCP>(o.p, r, tmin, tmax, t, sub, S.rcp_ok != 0);
     case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
     case YART_PRIM_MOVING_SPHERE: if (STATS) st.v[ST_PRIM]++; return moving_sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_MESH:
@@ -1382,7 +1449,12 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
   bool found = false;
   double closest = tmax;
+  uint32_t who = 0;  // obj << 3 | sub (the kernels without meshes)
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
+  // the plain list kernel (cornell's walls): the rects' divides share the ray's reciprocals
+  constexpr bool RCP = !HAS_MESH && !EXT;
+  AxisRcp rc;
+  if (RCP) rc = axis_rcp(r, tmin, S.rcp_ok != 0);
   for (uint32_t i = 0; i < S.n_objects; ++i) {
     const DevObject& o = uniform_at(S.objects, i);
     const uint32_t kind = o.kind, nxf = o.n_xf;
@@ -1402,15 +1474,23 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       const Ray lr = to_local(o, nxf, r);
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
-      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+      bool hit;
+      if (RCP && kind >= YART_PRIM_XY_RECT && kind <= YART_PRIM_YZ_RECT && o.rotated) {  // wave-uniform
+        const AxisRcp lrc = axis_rcp(lr, tmin, S.rcp_ok != 0);  // a RotateY turned the direction
+        hit = prim_t<HAS_MESH, STATS, RCP>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, &lrc);
+      } else {
+        hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                     : prim_t<HAS_MESH, STATS, RCP>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, &rc);
+      }
       if (hit) {
         closest = t;
-        id.obj = i; id.sub = sub; id.u = u; id.v = v;
+        if (HAS_MESH) { id.obj = i; id.sub = sub; id.u = u; id.v = v; }
+        else who = (i << 3) | sub;
         found = true;
       }
     }
   }
+  if (!HAS_MESH) { id.obj = who >> 3; id.sub = who & 7u; }
   id.t = closest;
   return found;
 }
@@ -1441,7 +1521,9 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
       rect_uv(a, bnd, lr, id.t, h);
     }
   } else if (kind == YART_PRIM_TRIANGLE) {
-    triangle_rec<EXT>(o.p, lr, id.t, id.u, id.v, h);
+    double u = id.u, v = id.v;  // the mesh kernels carry a triangle's u, v through the world pass
+    if (!HAS_MESH) triangle_uv(o.p, lr, u, v);
+    triangle_rec<EXT>(o.p, lr, id.t, u, v, h);
   } else if (kind == YART_PRIM_MOVING_SPHERE) {
     moving_sphere_rec<EXT>(o.p, lr, id.t, h);
   } else {
@@ -1465,15 +1547,17 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
   h.mat = o.material;
 }
 
-// World BVH walk (DevWorldNode; scenes without meshes): per lane, near child first, 32-slot
-// stack in LDS like the QBVH. The linear scan accepts an object iff its first root r_i >= t_min
-// satisfies r_i <= closest-so-far (every kind here is inclusive at t_max), so it returns the
-// minimum r_i, ties going to the LATER object; any visiting order that keeps (min t, max index)
-// returns the same winner, and the record is then rebuilt from it as before. Node culling is
-// an f32 slab test against the box grown by m = 2^-12 (node magnitude + |origin|) — f32 rounding
-// (~1e-7 relative) stays far inside m — over [t_min, closest] widened by 2^-10, so it never
-// drops a node holding a hit the scan would accept (ties included). Non-finite rays take the
-// list walk.
+// World BVH walk (DevWorldNode4; scenes without meshes): per lane over the 4-wide tree — the
+// binary SAH tree collapsed two levels per node (world_bvh.cpp), so a ray's chain of dependent node
+// reads is half as long (the random scene's walk waited on dependencies for 55 % of its wave
+// cycles) — nearest child first, 32-slot stack in LDS like the QBVH. The linear scan accepts an
+// object iff its first root r_i >= t_min satisfies r_i <= closest-so-far (every kind here is
+// inclusive at t_max), so it returns the minimum r_i, ties going to the LATER object; any visiting
+// order that keeps (min t, max index) returns the same winner, and the record is then rebuilt from
+// it as before. Node culling is an f32 slab test against the box grown by m = 2^-12 (node
+// magnitude + |origin|) — f32 rounding (~1e-7 relative) stays far inside m — over [t_min, closest]
+// widened by 2^-10, so it never drops a node holding a hit the scan would accept (ties included).
+// Non-finite rays take the list walk.
 template <bool STATS>
 __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
                                                   uint32_t* stk, Stats& st) {
@@ -1493,10 +1577,12 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   tlo = tlo - fabsf(tlo) * 0x1p-10f;
   bool found = false;
   double closest = tmax;
-  id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
-  // the walk carries node handles (DevWorldNode::pad[1]), read with the child boxes: descending
+  uint32_t who = 0;  // obj << 3 | sub; ties go to the later object: the larger word
+  id.u = 0.0; id.v = 0.0;
+  // the walk carries node handles (DevWorldNode4::handle), read with the child boxes: descending
   // and popping take a node without a dependent read of its own record
-  uint32_t hnd = S.world_nodes[0].pad[1];
+  const gfloat4p nodes = (gfloat4p)S.world_nodes;
+  uint32_t hnd = 0u;  // the root: inner node 0
   int cursor = 0;
   for (;;) {
     const uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
@@ -1509,9 +1595,9 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
         const double* sp = S.world_sph + 4 * (size_t)(first + k);
         if (STATS) st.v[ST_PRIM]++;
         double t;
-        if (sphere_t(sp, r, tmin, closest, t) && (!found || t < closest || i > id.obj)) {
+        if (sphere_t(sp, r, tmin, closest, t) && (!found || t < closest || (i << 3) > who)) {
           closest = t;
-          id.obj = i; id.sub = 0; id.u = 0.0; id.v = 0.0;
+          who = i << 3;
           found = true;
         }
       }
@@ -1523,44 +1609,59 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
         double t, u = 0.0, v = 0.0;
         uint32_t sub = 0;
         if (prim_t<false, STATS>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
-            (!found || t < closest || i > id.obj)) {
+            (!found || t < closest || (i << 3) > who)) {
           closest = t;
-          id.obj = i; id.sub = sub; id.u = u; id.v = v;
+          who = (i << 3) | sub;
           found = true;
         }
       }
     } else {
       float thi = (float)closest;
       thi = thi + fabsf(thi) * 0x1p-10f;
-      float entry[2];
-      bool hit[2];
-      uint32_t ch[2];
+      const gfloat4p N = nodes + 8 * (size_t)first;
+      float4 bmn[3], bmx[3];
+      bmn[0] = ld4(N, 0); bmn[1] = ld4(N, 1); bmn[2] = ld4(N, 2);
+      bmx[0] = ld4(N, 3); bmx[1] = ld4(N, 4); bmx[2] = ld4(N, 5);
+      const float4 mg = ld4(N, 6), hd = ld4(N, 7);
+      const float mk[4] = {mg.x, mg.y, mg.z, mg.w};
+      const uint32_t ch[4] = {__float_as_uint(hd.x), __float_as_uint(hd.y), __float_as_uint(hd.z), __float_as_uint(hd.w)};
+      // per child: the binary tree's test of that node (the same expression on the same box)
+      float key[4];  // entry of a hit child, +inf for a miss
+      uint32_t hc[4];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const DevWorldNode& C = S.world_nodes[first + c];
-        ch[c] = C.pad[1];
-        const float m = (C.mag + O) * 0x1p-12f;
+      for (int k = 0; k < 4; ++k) {
+        const float m = (mk[k] + O) * 0x1p-12f;
         float lo = tlo, hi = thi;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           if (use[j]) {
-            const float t0 = (C.bmin[j] - m - o[j]) * inv[j], t1 = (C.bmax[j] + m - o[j]) * inv[j];
+            const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
+            const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
+            const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
             lo = fmaxf(lo, fminf(t0, t1));
             hi = fminf(hi, fmaxf(t0, t1));
           }
         }
-        entry[c] = lo;
-        hit[c] = lo <= hi;
+        const bool hit = lo <= hi && ch[k] != kWorld4Empty;
+        key[k] = hit ? fminf(lo, 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
+        hc[k] = ch[k];
       }
       if (STATS) st.v[ST_NODES]++;
-      if (hit[0] && hit[1]) {
-        const bool n0 = entry[0] <= entry[1];
-        stk[cursor * 64] = n0 ? ch[1] : ch[0];
-        cursor++;
-        hnd = n0 ? ch[0] : ch[1];
-        pop = false;
-      } else if (hit[0] || hit[1]) {
-        hnd = hit[0] ? ch[0] : ch[1];
+      // nearest first: sort (key, handle) ascending (a 5-comparator network), take the first hit
+      // and push the other hits farthest first
+      auto cx = [&](int a, int b) {
+        const bool sw = key[b] < key[a];
+        const float ka = key[a], kb = key[b];
+        const uint32_t ha = hc[a], hb = hc[b];
+        key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;
+        hc[a] = sw ? hb : ha; hc[b] = sw ? ha : hb;
+      };
+      cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+      if (key[0] < INFINITY) {
+        if (key[3] < INFINITY) stk[(cursor++) * 64] = hc[3];
+        if (key[2] < INFINITY) stk[(cursor++) * 64] = hc[2];
+        if (key[1] < INFINITY) stk[(cursor++) * 64] = hc[1];
+        hnd = hc[0];
         pop = false;
       }
     }
@@ -1570,6 +1671,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       hnd = stk[cursor * 64];
     }
   }
+  id.obj = who >> 3; id.sub = who & 7u;
   id.t = closest;
   return found;
 }

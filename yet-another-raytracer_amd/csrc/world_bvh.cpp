@@ -216,13 +216,67 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     }
     n.pad[0] = all ? kWorldLeafSpheres : 0u;
   }
-  // Each node's handle (pad[1]): what the walk needs to take the node without reading its record
+  // Each leaf's handle (pad[1]): what the walk needs to take the node without reading its record
   // (the parent's child-box test reads the handle with the box, and the stack holds handles).
   for (DevWorldNode& n : out.nodes) {
     if (n.count > kWorldHandleMaxCount || n.first >= kWorldHandleFirstMask) return false;  // the list walk then
     n.pad[1] = (n.count << 28) | ((n.pad[0] & kWorldLeafSpheres) ? (1u << 27) : 0u) | n.first;
   }
-  return out.depth < (uint32_t)kStackSlots;
+  if (out.nodes[0].count != 0) return false;  // a single leaf: the list walk
+  // Collapse into the 4-wide tree: a 4-wide node takes a binary inner node's two children and, while
+  // it has fewer than four, replaces the inner one of largest box area by its own two children.
+  // Children keep the binary nodes' boxes (already rounded outward), so every box test is the one
+  // the binary walk made, and the walk's answer (min t, ties to the later object) is unchanged.
+  out.nodes4.clear();
+  out.depth4 = 0;
+  struct Job { uint32_t bin, slot, level; };
+  std::vector<Job> jobs{{0u, 0u, 1u}};
+  out.nodes4.emplace_back();
+  auto area = [&](uint32_t b) {
+    const DevWorldNode& n = out.nodes[b];
+    const double x = (double)n.bmax[0] - n.bmin[0], y = (double)n.bmax[1] - n.bmin[1], z = (double)n.bmax[2] - n.bmin[2];
+    return x * y + y * z + z * x;
+  };
+  while (!jobs.empty()) {
+    const Job j = jobs.back();
+    jobs.pop_back();
+    out.depth4 = std::max(out.depth4, j.level);
+    std::vector<uint32_t> kids{out.nodes[j.bin].first, out.nodes[j.bin].first + 1};
+    while (kids.size() < 4) {
+      int pick = -1;
+      double most = -1.0;
+      for (int k = 0; k < (int)kids.size(); ++k)
+        if (out.nodes[kids[k]].count == 0 && area(kids[k]) > most) { most = area(kids[k]); pick = k; }
+      if (pick < 0) break;
+      const uint32_t b = kids[pick];
+      kids[pick] = out.nodes[b].first;
+      kids.insert(kids.begin() + pick + 1, out.nodes[b].first + 1);
+    }
+    DevWorldNode4 q{};
+    for (int k = 0; k < 4; ++k) {
+      if (k >= (int)kids.size()) {
+        for (int a = 0; a < 3; ++a) { q.bmin[a][k] = INFINITY; q.bmax[a][k] = -INFINITY; }
+        q.mag[k] = 0.0f;
+        q.handle[k] = kWorld4Empty;
+        continue;
+      }
+      const DevWorldNode& c = out.nodes[kids[k]];
+      for (int a = 0; a < 3; ++a) { q.bmin[a][k] = c.bmin[a]; q.bmax[a][k] = c.bmax[a]; }
+      q.mag[k] = c.mag;
+      if (c.count) {
+        q.handle[k] = c.pad[1];  // a leaf
+      } else {
+        const uint32_t slot = (uint32_t)out.nodes4.size();  // an inner node: its own 4-wide node
+        if (slot >= kWorldHandleFirstMask) return false;
+        out.nodes4.emplace_back();
+        q.handle[k] = slot;
+        jobs.push_back({kids[k], slot, j.level + 1});
+      }
+    }
+    out.nodes4[j.slot] = q;
+  }
+  // the device walk pushes at most three entries per 4-wide level into its kStackSlots-deep stack
+  return out.depth < (uint32_t)kStackSlots && 3 * out.depth4 + 1 <= (uint32_t)kStackSlots;
 }
 
 }  // namespace yart_dev

@@ -9,7 +9,9 @@
 namespace yart_dev {
 
 struct BuiltWorld {
-  std::vector<DevWorldNode> nodes;  // root = nodes[0]
+  std::vector<DevWorldNode> nodes;  // the binary tree, root = nodes[0]
+  std::vector<DevWorldNode4> nodes4;  // the 4-wide tree the device walks, root = nodes4[0]
+  uint32_t depth4 = 0;              // its inner levels on the deepest root-to-leaf path
   std::vector<uint32_t> objs;       // leaf slots -> object index
   std::vector<double> sph;          // per leaf slot: centre xyz, radius of a plain sphere (else 0)
   uint32_t depth = 0;               // inner levels on the deepest root-to-leaf path
