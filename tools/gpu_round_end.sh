@@ -5,6 +5,8 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py with the driver's arguments
 #   prof_cornell  rocprofv3 trace + FETCH / WRITE / VALU / mix passes over bench.py (cornell, C2)
+#   prof_cornell_s1  the trace pass over bench.py --streams 1 (one frame in flight: the kernel's
+#            duration with no second stream's frame overlapping it)
 #   prof_cornell_more  stall / memory-instruction passes over bench.py (not in the default steps)
 #   prof_c4 / prof_c5  trace + FETCH / WRITE passes over the C4 / C5 frames tools/bench_configs.py
 #            times at --spp-scale 0.0625 (bunny 800x800x32, david 1920x1080x64)
@@ -13,7 +15,7 @@
 # Raw outputs under gpurun_out/; tools/summarize_profiles.py turns them into profiles/ files.
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$REPO/gpurun_out; mkdir -p "$OUT"; cd "$REPO"
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 run() {
   local name=$1 limit=$2; shift 2
   timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
@@ -21,13 +23,14 @@ run() {
   echo "== $name rc=$rc"; tail -n ${TAILN:-4} "$OUT/$name.log"
   [ $rc -eq 0 ] || { echo "stopping after rc=$rc"; exit $rc; }
 }
-STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_david prof_c4 prof_c5 configs"}
+STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_cornell_s1 prof_david prof_c4 prof_c5 configs"}
 for s in $STEPS; do
   case $s in
     pytest) run ${TAG}_gpu_tests 900 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
+    prof_cornell_s1) PFX=cornell_s1_ BENCH_ARGS="--steps 3 --warmup 1 --cpu-spp 0 --no-stats --streams 1" PASSES="trace" bash tools/profile.sh || exit 1 ;;
     prof_cornell_more) PFX=cornell_ PASSES="stall mem" bash tools/profile.sh || exit 1 ;;
     prof_david) PFX=david_ PROG="tools/render_once.py david 960 540 16 2" PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
     prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;

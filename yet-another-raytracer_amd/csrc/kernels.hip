@@ -557,21 +557,24 @@ __device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r,
 // q = RN(n r) corrected once by its exact fma residual (Markstein): bitwise RN(n / d[A]) for any
 // sign when |d[A]| is in [2^-300, 2^300] and |n| <= 2^300 (no scaling, overflow or underflow in the
 // steps). A quotient with |n| < 2^-600 may differ, but both are then below 2^-299, under t_min.
-// `ok` holds those ranges for the ray (|o| <= 2^299, and capi.cpp checks |k| <= 2^299 for every
-// rect and box coordinate of the scene, DevScene::rcp_ok) and t_min >= 2^-299; a lane without it
-// divides on the IEEE sequence (a rarely taken branch).
+// `ok` holds those ranges for every active lane that wants the query (|o| <= 2^299, and capi.cpp
+// checks |k| <= 2^299 for every rect and box coordinate of the scene, DevScene::rcp_ok, and
+// t_min >= 2^-299) — one ballot, so the rare wave with a lane outside them divides on the IEEE
+// sequence for all its lanes: a uniform branch. (Per lane, the compiler computed both quotients
+// and selected, which cost more than the divide alone: cornell -5 %.)
 struct AxisRcp { double r[3]; bool ok; };
-__device__ __forceinline__ AxisRcp axis_rcp(const Ray& ray, double tmin, bool scene_ok) {
+__device__ __forceinline__ AxisRcp axis_rcp(const Ray& ray, double tmin, bool scene_ok, bool want = true) {
   AxisRcp q;
   const double* o = &ray.o.x;
   const double* d = &ray.d.x;
-  bool ok = scene_ok && tmin >= 0x1p-299;
+  bool ok = tmin >= 0x1p-299;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     ok = ok && fabs(d[j]) >= 0x1p-300 && fabs(d[j]) <= 0x1p300 && fabs(o[j]) <= 0x1p299;
     q.r[j] = rcp_core(d[j]);
+    asm volatile("" : "+v"(q.r[j]));  // formed once per pass: left alone, it was re-formed at every rect
   }
-  q.ok = ok;
+  q.ok = scene_ok && __ballot(want && !ok) == 0ull;
   return q;
 }
 __device__ __forceinline__ double quo_rcp(double n, double d, double r) {  // RN(n / d) in AxisRcp's ranges
@@ -588,9 +591,8 @@ __device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmi
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
-  if (RCP) {
+  if (RCP && rc->ok) {  // wave-uniform
     t = quo_rcp(num, den, rc->r[A]);
-    if (!rc->ok) t = num / den;
   } else {
     t = num / den;
   }
@@ -1454,7 +1456,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
   // the plain list kernel (cornell's walls): the rects' divides share the ray's reciprocals
   constexpr bool RCP = !HAS_MESH && !EXT;
   AxisRcp rc;
-  if (RCP) rc = axis_rcp(r, tmin, S.rcp_ok != 0);
+  if (RCP) rc = axis_rcp(r, tmin, S.rcp_ok != 0, want);
   for (uint32_t i = 0; i < S.n_objects; ++i) {
     const DevObject& o = uniform_at(S.objects, i);
     const uint32_t kind = o.kind, nxf = o.n_xf;
