@@ -126,7 +126,6 @@ DevObject to_dev(const yart_object& o) {
     }
   }
   for (int k = 0; k < 24; ++k) d.p[k] = o.p[k];
-  for (uint32_t l = 0; l < d.n_xf && l < (uint32_t)kMaxXforms; ++l) d.rotated |= d.xf_kind[l] == YART_XF_ROTATE_Y;
   return d;
 }
 
@@ -336,14 +335,6 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
   ds.has_mesh = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_mesh |= d->objects[i].kind == YART_PRIM_MESH;
-  // the shared-reciprocal rect divides (kernels.hip AxisRcp) need every rect / box coordinate (and
-  // so every numerator k - o) within 2^299
-  ds.rcp_ok = 1;
-  for (uint32_t i = 0; i < d->n_objects; ++i) {
-    const yart_object& o = d->objects[i];
-    if (o.kind >= YART_PRIM_XY_RECT && o.kind <= YART_PRIM_BOX)
-      for (int k = 0; k < (o.kind == YART_PRIM_BOX ? 6 : 5); ++k) ds.rcp_ok &= std::fabs(o.p[k]) <= 0x1p299 ? 1u : 0u;
-  }
   ds.has_ext = 0;
   for (uint32_t i = 0; i < d->n_objects; ++i) ds.has_ext |= d->objects[i].n_xforms && d->objects[i].xforms[0].kind == YART_XF_MEDIUM;
   for (uint32_t i = 0; i < d->n_materials; ++i) ds.has_ext |= d->materials[i].kind == YART_MAT_ISOTROPIC;

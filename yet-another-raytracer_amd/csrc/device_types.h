@@ -1,7 +1,7 @@
 // device_types.h — HBM layout of a scene on one MI355X (shared by the host side of libyart and
 // the kernels). Everything the per-sample loop reads is resident; nothing is rebuilt per frame.
 //
-//  DevObject   world / light list entries in list order (hittable.rs:47-123). 328 B each; a wave
+//  DevObject   world / light list entries in list order (hittable.rs:47-123). 320 B each; a wave
 //              walks the list with a wave-uniform index, so the fields come in on the scalar path.
 //  DevMaterial material table (material.rs), 64 B.
 //  DevTexture  36-bin spectra precomputed from RGB with the Smits basis (color.rs:54-90): the
@@ -31,8 +31,6 @@ struct DevObject {
   uint32_t xf_kind[kMaxXforms];
   double xf[kMaxXforms][3];  // TRANSLATE: offset; ROTATE_Y: sin, cos (hittable.rs:173-176)
   double p[24];
-  uint32_t rotated;  // a RotateY wrapper turns the ray's direction (the shared reciprocals do not apply)
-  uint32_t pad_;
 };
 
 struct DevMaterial {
@@ -148,7 +146,6 @@ struct DevScene {
   uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
   uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
-  uint32_t rcp_ok;   // every rect / box coordinate within 2^299: the shared-reciprocal divides apply (kernels.hip AxisRcp)
 };
 
 }  // namespace yart_dev

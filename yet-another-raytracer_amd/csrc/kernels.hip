@@ -551,51 +551,13 @@ __device__ __forceinline__ void moving_sphere_rec(const double* p, const Ray& r,
   h.t = t; h.p = pt;
 }
 
-// Shared reciprocals of a ray's direction for the rect and box-face tests of one world pass: the
-// rects of one axis divide by the same d[A], and the IEEE quotient's first half (scale, v_rcp_f64,
-// two Newton steps) depends on the denominator only. With r = rcp_core(d[A]), the quotient is
-// q = RN(n r) corrected once by its exact fma residual (Markstein): bitwise RN(n / d[A]) for any
-// sign when |d[A]| is in [2^-300, 2^300] and |n| <= 2^300 (no scaling, overflow or underflow in the
-// steps). A quotient with |n| < 2^-600 may differ, but both are then below 2^-299, under t_min.
-// `ok` holds those ranges for every active lane that wants the query (|o| <= 2^299, and capi.cpp
-// checks |k| <= 2^299 for every rect and box coordinate of the scene, DevScene::rcp_ok, and
-// t_min >= 2^-299) — one ballot, so the rare wave with a lane outside them divides on the IEEE
-// sequence for all its lanes: a uniform branch. (Per lane, the compiler computed both quotients
-// and selected, which cost more than the divide alone: cornell -5 %.)
-struct AxisRcp { double r[3]; bool ok; };
-__device__ __forceinline__ AxisRcp axis_rcp(const Ray& ray, double tmin, bool scene_ok, bool want = true) {
-  AxisRcp q;
-  const double* o = &ray.o.x;
-  const double* d = &ray.d.x;
-  bool ok = tmin >= 0x1p-299;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    ok = ok && fabs(d[j]) >= 0x1p-300 && fabs(d[j]) <= 0x1p300 && fabs(o[j]) <= 0x1p299;
-    q.r[j] = rcp_core(d[j]);
-    asm volatile("" : "+v"(q.r[j]));  // formed once per pass: left alone, it was re-formed at every rect
-  }
-  q.ok = scene_ok && __ballot(want && !ok) == 0ull;
-  return q;
-}
-__device__ __forceinline__ double quo_rcp(double n, double d, double r) {  // RN(n / d) in AxisRcp's ranges
-  const double q = n * r;
-  const double remn = __builtin_fma(d, q, -n);
-  return __builtin_fma(-remn, r, q);
-}
-
-// aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k. RCP: t from the ray's shared
-// reciprocal (rc, above).
-template <int A, int B, int CC, bool RCP = false>
-__device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t,
-                                       const AxisRcp* rc = nullptr) {
+// aarect.rs: A = plane axis, B/C = in-plane axes; p = b0 b1 c0 c1 k.
+template <int A, int B, int CC>
+__device__ __forceinline__ bool rect_t(const double* p, const Ray& r, double tmin, double tmax, double& t) {
   const double* o = &r.o.x;
   const double* d = &r.d.x;
   const double num = p[4] - o[A], den = d[A];
-  if (RCP && rc->ok) {  // wave-uniform
-    t = quo_rcp(num, den, rc->r[A]);
-  } else {
-    t = num / den;
-  }
+  t = num / den;
   if (t < tmin || t > tmax) return false;
   double x = o[B] + t * d[B];
   double y = o[CC] + t * d[CC];
@@ -660,25 +622,20 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
 
 // BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
 // 4-5 yz, so the face's plane axis is 2 - face / 2.
-// RCP: the six faces divide by the box's (local) ray's shared reciprocals, formed here once.
-template <bool RCP = false>
-__device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face,
-                                      bool scene_ok = false) {
+__device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face) {
   if (!box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
   double closest = tmax, tt;
   double s[5];
-  AxisRcp rc;
-  if (RCP) rc = axis_rcp(r, tmin, scene_ok);
   s[0] = p[0]; s[1] = p[3]; s[2] = p[1]; s[3] = p[4];
-  s[4] = p[2]; if (rect_t<2, 0, 1, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 0; found = true; }
-  s[4] = p[5]; if (rect_t<2, 0, 1, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 1; found = true; }
+  s[4] = p[2]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 0; found = true; }
+  s[4] = p[5]; if (rect_t<2, 0, 1>(s, r, tmin, closest, tt)) { closest = tt; face = 1; found = true; }
   s[2] = p[2]; s[3] = p[5];
-  s[4] = p[1]; if (rect_t<1, 0, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 2; found = true; }
-  s[4] = p[4]; if (rect_t<1, 0, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 3; found = true; }
+  s[4] = p[1]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 2; found = true; }
+  s[4] = p[4]; if (rect_t<1, 0, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 3; found = true; }
   s[0] = p[1]; s[1] = p[4];
-  s[4] = p[0]; if (rect_t<0, 1, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 4; found = true; }
-  s[4] = p[3]; if (rect_t<0, 1, 2, RCP>(s, r, tmin, closest, tt, &rc)) { closest = tt; face = 5; found = true; }
+  s[4] = p[0]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 4; found = true; }
+  s[4] = p[3]; if (rect_t<0, 1, 2>(s, r, tmin, closest, tt)) { closest = tt; face = 5; found = true; }
   t = closest;
   return found;
 }
@@ -1355,25 +1312,22 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 }
 
 // ------------------------------------------------------------------------ world hit
-// Which primitive of the world list won, and where: enough to rebuild its record exactly.
 // Which primitive of the world list won, and where: enough to rebuild its record exactly. In the
 // list and world-BVH kernels the world pass keeps t and one word, obj << 3 | sub (sub = a box face;
 // every update is then one 64-bit and one 32-bit select), and the record recomputes a triangle's
 // u, v; the mesh kernels carry u, v and the triangle (a mesh hit's walk result) through the pass.
 struct HitId { double t, u, v; uint32_t obj, sub; };
 
-// RCP: rects divide by the shared reciprocals `rc` of the ray they are given (the caller's
-// world-pass reciprocals, or the object's own when a RotateY changed the direction).
-template <bool HAS_MESH, bool STATS, bool RCP = false>
+template <bool HAS_MESH, bool STATS>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
                                        double tmin, double tmax, double& t, uint32_t& sub, double& u, double& v,
-                                       uint32_t* stk, Stats& st, const AxisRcp* rc = nullptr) {
+                                       uint32_t* stk, Stats& st) {
   switch (kind) {
     case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_t(o.p, r, tmin, tmax, t);
-    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1, RCP>(o.p, r, tmin, tmax, t, rc);
-    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2, RCP>(o.p, r, tmin, tmax, t, rc);
-    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2, RCP>(o.p, r, tmin, tmax, t, rc);
-    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t<RCP>(o.p, r, tmin, tmax, t, sub, S.rcp_ok != 0);
+    case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2>(o.p, r, tmin, tmax, t);
+    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t(o.p, r, tmin, tmax, t, sub);
     case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
     case YART_PRIM_MOVING_SPHERE: if (STATS) st.v[ST_PRIM]++; return moving_sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_MESH:
@@ -1453,10 +1407,6 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
   double closest = tmax;
   uint32_t who = 0;  // obj << 3 | sub (the kernels without meshes)
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
-  // the plain list kernel (cornell's walls): the rects' divides share the ray's reciprocals
-  constexpr bool RCP = !HAS_MESH && !EXT;
-  AxisRcp rc;
-  if (RCP) rc = axis_rcp(r, tmin, S.rcp_ok != 0, want);
   for (uint32_t i = 0; i < S.n_objects; ++i) {
     const DevObject& o = uniform_at(S.objects, i);
     const uint32_t kind = o.kind, nxf = o.n_xf;
@@ -1476,14 +1426,8 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       const Ray lr = to_local(o, nxf, r);
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
-      bool hit;
-      if (RCP && kind >= YART_PRIM_XY_RECT && kind <= YART_PRIM_YZ_RECT && o.rotated) {  // wave-uniform
-        const AxisRcp lrc = axis_rcp(lr, tmin, S.rcp_ok != 0);  // a RotateY turned the direction
-        hit = prim_t<HAS_MESH, STATS, RCP>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, &lrc);
-      } else {
-        hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                     : prim_t<HAS_MESH, STATS, RCP>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, &rc);
-      }
+      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
+                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
       if (hit) {
         closest = t;
         if (HAS_MESH) { id.obj = i; id.sub = sub; id.u = u; id.v = v; }
