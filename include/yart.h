@@ -407,6 +407,18 @@ typedef struct yart_qbvh_build_info {
 int yart_qbvh_build(const float* positions, const double* normals, uint32_t n_triangles, uint32_t flags,
                     yart_qbvh_build_info* out);
 
+/* The world BVH of a scene description on its own (no device): the binary SAH tree and the 4-wide
+ * tree the device walks, built exactly as yart_scene_create builds them (whatever the object count;
+ * built = 0 when some object has no box: meshes, media, moving spheres), then the 4-wide tree's
+ * structural check (world_bvh.cpp check_world4: every object in exactly one leaf, every child box
+ * holding the objects below it, depth within the walk's stack; valid = 1, or the reason in
+ * yart_last_error). digest: FNV-1a 64 over the 4-wide nodes, leaf slots and sphere records. */
+typedef struct yart_world_bvh_info {
+  uint32_t built, nodes, depth, nodes4, depth4, valid;
+  uint64_t digest;
+} yart_world_bvh_info;
+int yart_world_bvh_build(const yart_scene_desc* desc, yart_world_bvh_info* out);
+
 /* Test probes (device side of the parity tests). */
 /* The per-sample random stream: n draws of gen::<f64>() for (pixel, sample). */
 int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n,

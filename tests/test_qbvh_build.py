@@ -65,3 +65,56 @@ def test_walk_tree_structure(meshes, name):
     assert w["nodes"] == MESHES[name][1]  # the reference tree's shape is unchanged
     assert yart.qbvh_build(pos, nrm, yart.QBVH_WALK | yart.QBVH_SERIAL)["digest"] == w["digest"]
     assert yart.qbvh_build(pos, nrm)["digest"] != w["digest"]
+
+
+@pytest.mark.parametrize("scene", ["random-scene", "cornell-box", "three-spheres", "two-spheres"])
+def test_world_bvh_4wide_structure(scene):
+    """The world BVH the no-mesh kernels walk (world_bvh.cpp), built on the host as scene creation
+    builds it: the binary SAH tree collapsed into 4-wide nodes with every object in exactly one
+    leaf, every child box holding the world box of each object below it (wrappers included) and
+    the depth within the walk's 32-slot stack (check_world4). Deterministic: the same digest twice."""
+    p = yart.Preset(scene)
+    a = yart.world_bvh_build(p.desc)
+    assert a["built"] == 1 and a["valid"] == 1
+    assert a["nodes4"] < a["nodes"] and 2 * a["depth4"] >= a["depth"] and a["depth4"] <= a["depth"]
+    assert yart.world_bvh_build(p.desc)["digest"] == a["digest"]
+
+
+def test_world_bvh_4wide_structure_on_mixed_synthetic_lists():
+    """Random lists of plain, hollow and translated spheres, rects, rotated / translated boxes and
+    triangles, 1 to 600 objects: the 4-wide tree passes its structural check for every list of more
+    than one leaf (a list the SAH keeps in one leaf stays on the linear walk), and a list holding a moving sphere is
+    left to the linear walk (built = 0)."""
+    import numpy as np
+    import oracle_lib as O
+    from yart import abi
+    rng = np.random.default_rng(31)
+    for n in [1, 2, 3, 4, 5, 16, 17, 63, 64, 65, 257, 600]:
+        b = O.DescBuilder()
+        m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+        for k in range(n):
+            c = tuple(float(x) for x in rng.uniform(-50, 50, 3))
+            kind = k % 6
+            if kind == 0:
+                b.obj(abi.PRIM_SPHERE, m, c + (float(rng.uniform(0.1, 3)),))
+            elif kind == 1:
+                b.obj(abi.PRIM_SPHERE, m, (0.0, 0.0, 0.0, -float(rng.uniform(0.1, 3))), xforms=[(abi.XF_TRANSLATE, c)])
+            elif kind == 2:
+                b.obj(abi.PRIM_XZ_RECT, m, (c[0], c[0] + 4.0, c[2], c[2] + 3.0, c[1]))
+            elif kind == 3:
+                b.obj(abi.PRIM_BOX, m, (0.0, 0.0, 0.0, 2.0, 5.0, 1.0),
+                      xforms=[(abi.XF_TRANSLATE, c), (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))])
+            elif kind == 4:
+                v = rng.uniform(-2, 2, 9) + np.tile(c, 3)
+                b.obj(abi.PRIM_TRIANGLE, m, tuple(float(x) for x in v) + (0.0, 1.0, 0.0) * 3 + (0.0,) * 6)
+            else:
+                b.obj(abi.PRIM_YZ_RECT, m, (c[1], c[1] + 2.0, c[2], c[2] + 2.0, c[0]), xforms=[(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))])
+        info = yart.world_bvh_build(b.desc())
+        assert info["built"] == 0 or info["valid"] == 1, (n, info)
+        assert info["built"] == 1 or n <= 4, (n, info)  # a single leaf stays on the linear walk
+    b = O.DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    for k in range(20):
+        b.obj(abi.PRIM_SPHERE, m, (float(k), 0.0, 0.0, 0.4))
+    b.obj(abi.PRIM_MOVING_SPHERE, m, (0.0, 1.0, 0.0, 1.0, 1.0, 0.0, 0.0, 1.0, 0.3))
+    assert yart.world_bvh_build(b.desc())["built"] == 0

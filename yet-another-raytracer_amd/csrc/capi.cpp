@@ -428,6 +428,33 @@ int yart_qbvh_build(const float* positions, const double* normals, uint32_t n, u
   return ok();
 }
 
+int yart_world_bvh_build(const yart_scene_desc* d, yart_world_bvh_info* out) {
+  if (!d || !out || (d->n_objects && !d->objects)) return fail(YART_ERR_INVALID, "null argument");
+  std::memset(out, 0, sizeof *out);
+  std::vector<DevObject> objs;
+  for (uint32_t i = 0; i < d->n_objects; ++i) objs.push_back(to_dev(d->objects[i]));
+  BuiltWorld w;
+  if (objs.empty() || !build_world_bvh(objs, w)) return ok();  // built = 0: the list walk
+  out->built = 1;
+  out->nodes = (uint32_t)w.nodes.size();
+  out->depth = w.depth;
+  out->nodes4 = (uint32_t)w.nodes4.size();
+  out->depth4 = w.depth4;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+  auto mix = [&h](const void* p, size_t len) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < len; ++i) { h ^= c[i]; h *= 1099511628211ull; }
+  };
+  mix(w.nodes4.data(), w.nodes4.size() * sizeof(DevWorldNode4));
+  mix(w.objs.data(), w.objs.size() * sizeof(uint32_t));
+  mix(w.sph.data(), w.sph.size() * sizeof(double));
+  out->digest = h;
+  std::string err;
+  if (!check_world4(objs, w, err)) return fail(YART_ERR_UNSUPPORTED, "world BVH check: " + err);
+  out->valid = 1;
+  return ok();
+}
+
 int yart_scene_get_info(const yart_scene* s, yart_scene_info* out) {
   if (!s || !out) return fail(YART_ERR_INVALID, "null argument");
   *out = s->info;

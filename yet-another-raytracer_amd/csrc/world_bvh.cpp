@@ -6,6 +6,7 @@
 #include <numeric>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 namespace yart_dev {
 
@@ -277,6 +278,79 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
   }
   // the device walk pushes at most three entries per 4-wide level into its kStackSlots-deep stack
   return out.depth < (uint32_t)kStackSlots && 3 * out.depth4 + 1 <= (uint32_t)kStackSlots;
+}
+
+bool check_world4(const std::vector<DevObject>& objs, const BuiltWorld& w, std::string& err) {
+  if (w.nodes4.empty()) { err = "no 4-wide nodes"; return false; }
+  std::vector<int> seen(objs.size(), 0);
+  struct Item { uint32_t node, level; };
+  std::vector<Item> todo{{0u, 1u}};
+  std::vector<char> visited(w.nodes4.size(), 0);
+  uint32_t depth = 0;
+  while (!todo.empty()) {
+    const Item it = todo.back();
+    todo.pop_back();
+    if (it.node >= w.nodes4.size() || visited[it.node]) { err = "node reached twice or out of range"; return false; }
+    visited[it.node] = 1;
+    depth = std::max(depth, it.level);
+    const DevWorldNode4& q = w.nodes4[it.node];
+    int kids = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t h = q.handle[k];
+      if (h == kWorld4Empty) {
+        for (int a = 0; a < 3; ++a)
+          if (!(q.bmin[a][k] == INFINITY && q.bmax[a][k] == -INFINITY)) { err = "empty slot with a box"; return false; }
+        continue;
+      }
+      ++kids;
+      const uint32_t count = h >> 28, first = h & (kWorldHandleFirstMask - 1u);
+      // everything below the child lies inside the child's box (the boxes the binary walk tested)
+      std::vector<uint32_t> below;
+      if (count) {
+        if ((size_t)first + count > w.objs.size()) { err = "leaf range out of bounds"; return false; }
+        for (uint32_t j = 0; j < count; ++j) below.push_back(w.objs[first + j]);
+      } else {
+        if (h >= w.nodes4.size()) { err = "inner handle out of range"; return false; }
+        todo.push_back({h, it.level + 1});
+        std::vector<uint32_t> stack{h};
+        while (!stack.empty()) {
+          const DevWorldNode4& c = w.nodes4[stack.back()];
+          stack.pop_back();
+          for (int kk = 0; kk < 4; ++kk) {
+            const uint32_t hh = c.handle[kk];
+            if (hh == kWorld4Empty) continue;
+            if (hh >> 28) {
+              for (uint32_t j = 0; j < (hh >> 28); ++j) below.push_back(w.objs[(hh & (kWorldHandleFirstMask - 1u)) + j]);
+            } else {
+              if (hh >= w.nodes4.size()) { err = "inner handle out of range"; return false; }
+              stack.push_back(hh);
+            }
+          }
+        }
+      }
+      for (uint32_t i : below) {
+        if (i >= objs.size()) { err = "object index out of range"; return false; }
+        double lo[3], hi[3];
+        if (!world_bounds(objs[i], lo, hi)) { err = "object without a box in the tree"; return false; }
+        for (int a = 0; a < 3; ++a)
+          if (!((double)q.bmin[a][k] <= lo[a] && hi[a] <= (double)q.bmax[a][k])) { err = "child box does not hold an object below it"; return false; }
+      }
+      if (count) {
+        const bool spheres = ((h >> 27) & 1u) != 0;
+        for (uint32_t j = 0; j < count; ++j) {
+          const DevObject& o = objs[w.objs[first + j]];
+          ++seen[w.objs[first + j]];
+          if (spheres && !(o.kind == YART_PRIM_SPHERE && o.n_xf == 0)) { err = "sphere leaf holding another kind"; return false; }
+        }
+      }
+    }
+    if (kids < 2) { err = "inner node with fewer than two children"; return false; }
+  }
+  for (size_t i = 0; i < seen.size(); ++i)
+    if (seen[i] != 1) { err = "object " + std::to_string(i) + " in " + std::to_string(seen[i]) + " leaves"; return false; }
+  if (depth != w.depth4) { err = "depth4 does not match the tree"; return false; }
+  if (3 * depth + 1 > (uint32_t)kStackSlots) { err = "deeper than the walk's stack"; return false; }
+  return true;
 }
 
 }  // namespace yart_dev

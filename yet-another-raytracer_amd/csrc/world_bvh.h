@@ -1,6 +1,7 @@
 // world_bvh.h — host-side build of the world BVH (DevWorldNode) over a scene's object list.
 #pragma once
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "device_types.h"
@@ -28,5 +29,11 @@ bool world_bounds(const DevObject& o, double lo[3], double hi[3]);
 // magnitude and rounded outward to f32. Any tree gives the linear scan's answer (the walk keeps
 // min t, ties to the later object: kernels.hip world_closest_bvh). false if some object has no box.
 bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah = true);
+
+// The 4-wide tree's structure: every object in exactly one leaf reachable from the root, every
+// child box holding the world box of each object below it, sphere leaves holding plain spheres,
+// empty slots without a box, at least two children per node, depth4 the tree's and within the
+// walk's 32-slot stack. false with a reason in err.
+bool check_world4(const std::vector<DevObject>& objs, const BuiltWorld& w, std::string& err);
 
 }  // namespace yart_dev

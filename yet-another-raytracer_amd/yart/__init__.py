@@ -110,6 +110,7 @@ def load_device():
     if hasattr(L, "yart_multi_query"):  # diagnostics only (bench.py's watchdog); absent from older A/B builds
         _sig(L, "yart_multi_query", I, P, P, P)
     _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
+    _sig(L, "yart_world_bvh_build", I, C.POINTER(abi.SceneDesc), C.POINTER(abi.WorldBvhInfo))
     _sig(L, "yart_debug_set_option", I, I, C.c_int64)
     _sig(L, "yart_debug_get_option", I, I, C.POINTER(C.c_int64))
     _dev = L
@@ -305,6 +306,14 @@ def qbvh_build(positions, normals, flags=0):
     info = abi.QbvhBuildInfo()
     _check_dev(load_device().yart_qbvh_build(_ptr(positions), _ptr(normals), len(positions), flags, C.byref(info)))
     return {k: getattr(info, k) for k, _ in info._fields_ if "reserved" not in k}
+
+
+def world_bvh_build(desc):
+    """Host-only world BVH build of a scene description (yart_world_bvh_build): the binary and
+    4-wide trees as scene creation builds them, and the 4-wide tree's structural check."""
+    info = abi.WorldBvhInfo()
+    _check_dev(load_device().yart_world_bvh_build(desc, C.byref(info)))
+    return {k: getattr(info, k) for k, _ in info._fields_}
 
 
 def finalize_rgba8(xyz_sum, spp, device=0):

@@ -80,6 +80,11 @@ class QbvhBuildInfo(C.Structure):
                 ("walk_valid", C.c_uint32), ("walk_reserved", C.c_uint32), ("walk_build_ms", C.c_double)]
 
 
+class WorldBvhInfo(C.Structure):
+    _fields_ = [("built", C.c_uint32), ("nodes", C.c_uint32), ("depth", C.c_uint32), ("nodes4", C.c_uint32),
+                ("depth4", C.c_uint32), ("valid", C.c_uint32), ("digest", C.c_uint64)]
+
+
 class RenderStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("leaf_tris", C.c_uint64),
@@ -118,6 +123,7 @@ DEVICE_SYMBOLS = [
     "yart_debug_set_option",
     "yart_debug_get_option",
     "yart_multi_query",
+    "yart_world_bvh_build",
     "yart_shard_packed_len", "yart_render_packed_async", "yart_comm_unique_id", "yart_comm_init_rank",
     "yart_comm_init_all", "yart_comm_destroy", "yart_gather_frame_async", "yart_multi_create", "yart_render_multi",
     "yart_multi_last_timing", "yart_multi_destroy", "yart_qbvh_build", "yart_render_multi_async",
