@@ -110,7 +110,8 @@ def load_device():
     if hasattr(L, "yart_multi_query"):  # diagnostics only (bench.py's watchdog); absent from older A/B builds
         _sig(L, "yart_multi_query", I, P, P, P)
     _sig(L, "yart_qbvh_build", I, P, P, U32, U32, C.POINTER(abi.QbvhBuildInfo))
-    _sig(L, "yart_world_bvh_build", I, C.POINTER(abi.SceneDesc), C.POINTER(abi.WorldBvhInfo))
+    if hasattr(L, "yart_world_bvh_build"):  # host-side check only; absent from older A/B builds
+        _sig(L, "yart_world_bvh_build", I, C.POINTER(abi.SceneDesc), C.POINTER(abi.WorldBvhInfo))
     _sig(L, "yart_debug_set_option", I, I, C.c_int64)
     _sig(L, "yart_debug_get_option", I, I, C.POINTER(C.c_int64))
     _dev = L
