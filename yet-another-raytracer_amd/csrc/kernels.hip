@@ -2647,9 +2647,75 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
   }
 }
 
+// ------------------------------------------------------------------------- launchers
+hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t stream) {
+  const uint32_t n = a.n_blocks * 64;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_accumulate, dim3((n + 255) / 256), dim3(256), 0, stream, a, first_pass ? 1 : 0);
+  return hipGetLastError();
+}
+hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream) {
+  const bool dyn = a.scratch != nullptr;  // stats launches are always fused (see capi.cpp)
+  const uint32_t units = a.n_blocks * a.n_chunks;
+  const uint32_t grid = ((dyn && a.waves < units ? a.waves : units) + 3) / 4;
+  if (grid == 0) return hipSuccess;
+#define YART_LAUNCH(MESH, BVH, EXT)                                                                            \
+  do {                                                                                                        \
+    if (stats) hipLaunchKernelGGL((k_render<MESH, BVH, true, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);  \
+    else if (dyn) hipLaunchKernelGGL((k_render<MESH, BVH, false, true, EXT>), dim3(grid), dim3(256), 0, stream, s, a); \
+    else hipLaunchKernelGGL((k_render<MESH, BVH, false, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);        \
+  } while (0)
+  if (s.has_mesh) {
+    if (s.has_ext) YART_LAUNCH(true, false, true); else YART_LAUNCH(true, false, false);
+  } else if (s.world_nodes) {
+    if (s.has_ext) YART_LAUNCH(false, true, true); else YART_LAUNCH(false, true, false);  // noise textures only
+  } else {
+    if (s.has_ext) YART_LAUNCH(false, false, true); else YART_LAUNCH(false, false, false);
+  }
+#undef YART_LAUNCH
+  return hipGetLastError();
+}
+hipError_t launch_wf_shade(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
+  hipLaunchKernelGGL(k_wf_shade, dim3(w.pool / 256), dim3(256), 0, stream, s, a, w);
+  return hipGetLastError();
+}
+hipError_t launch_wf_trace(const DevScene& s, const RenderArgs& a, const WfArgs& w, hipStream_t stream) {
+  const uint32_t batches = w.pool / 64;
+  const uint32_t grid = batches;
+  if (s.deep) hipLaunchKernelGGL(k_wf_trace<kDeepSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
+  else hipLaunchKernelGGL(k_wf_trace<kCoopSlots>, dim3(grid), dim3(64), 0, stream, s, a, w);
+  return hipGetLastError();
+}
+hipError_t launch_unpack_shards(const double* recv, uint32_t shards, size_t stride, uint32_t w, uint32_t h, double* frame,
+                                hipStream_t stream) {
+  const uint32_t n = w * h;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_shards, dim3((n + 255) / 256), dim3(256), 0, stream, recv, shards, stride, w, h, frame);
+  return hipGetLastError();
+}
+hipError_t launch_intersect(const DevScene& s, const double* rays, uint32_t n, double* hits, int32_t* obj,
+                            hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (s.deep) hipLaunchKernelGGL(k_intersect<kDeepSlots>, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
+  else hipLaunchKernelGGL(k_intersect<kCoopSlots>, dim3((n + 255) / 256), dim3(256), 0, stream, s, rays, n, hits, obj);
+  return hipGetLastError();
+}
+hipError_t launch_finalize(const double* xyz, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba, hipStream_t stream) {
+  const uint32_t n = w * h;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, stream, xyz, w, h, spp, rgba);
+  return hipGetLastError();
+}
+hipError_t launch_probe_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_probe_rng, dim3(1), dim3(64), 0, stream, seed, pixel, sample, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_probe_math(int op, const double* a, const double* b, uint32_t n, double* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_math, dim3((n + 255) / 256), dim3(256), 0, stream, op, a, b, n, out);
+  return hipGetLastError();
+}
 
-template __global__ void k_render<true, false, false, true, false>(DevScene, RenderArgs);
-template __global__ void k_wf_trace<64>(DevScene, RenderArgs, WfArgs);
 }  // namespace yart_dev
 
 extern "C" int yart_debug_force_rewalk(int device, int on) {
