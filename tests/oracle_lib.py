@@ -231,3 +231,32 @@ class DescBuilder:
         d.background = (C.c_double * 3)(*self.background)
         self._desc = d
         return C.pointer(d)
+
+
+def mixed_list_desc(n, seed, spread=50.0):
+    """A scene description of n mixed list entries (test infrastructure): plain and hollow
+    translated spheres, XZ rects, translated + rotated boxes, triangles and flipped YZ rects at
+    random places within +-spread, one Lambertian material. The world BVH's structural and parity
+    tests run over these."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    b = DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    for k in range(n):
+        c = tuple(float(x) for x in rng.uniform(-spread, spread, 3))
+        kind = k % 6
+        if kind == 0:
+            b.obj(abi.PRIM_SPHERE, m, c + (float(rng.uniform(0.1, 3)),))
+        elif kind == 1:
+            b.obj(abi.PRIM_SPHERE, m, (0.0, 0.0, 0.0, -float(rng.uniform(0.1, 3))), xforms=[(abi.XF_TRANSLATE, c)])
+        elif kind == 2:
+            b.obj(abi.PRIM_XZ_RECT, m, (c[0], c[0] + 4.0, c[2], c[2] + 3.0, c[1]))
+        elif kind == 3:
+            b.obj(abi.PRIM_BOX, m, (0.0, 0.0, 0.0, 2.0, 5.0, 1.0),
+                  xforms=[(abi.XF_TRANSLATE, c), (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))])
+        elif kind == 4:
+            v = rng.uniform(-2, 2, 9) + np.tile(c, 3)
+            b.obj(abi.PRIM_TRIANGLE, m, tuple(float(x) for x in v) + (0.0, 1.0, 0.0) * 3 + (0.0,) * 6)
+        else:
+            b.obj(abi.PRIM_YZ_RECT, m, (c[1], c[1] + 2.0, c[2], c[2] + 2.0, c[0]), xforms=[(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))])
+    return b

@@ -312,6 +312,24 @@ def test_world_bvh_forced_on_matches_linear_scan(dev, scene, opt):
                                   O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
 
 
+@pytest.mark.parametrize("n", [17, 64, 257, 600])
+def test_world_bvh_4wide_mixed_lists_match_linear_scan(dev, n):
+    """The 4-wide world BVH (forced on) over random mixed lists — plain, hollow and translated
+    spheres, rects, translated + rotated boxes, triangles, flipped rects (oracle_lib.mixed_list_desc,
+    the lists test_qbvh_build checks structurally): 100k random rays from inside and outside the
+    cloud, closest hits bitwise the oracle's linear HittableList scan."""
+    b = O.mixed_list_desc(n, seed=31 + n, spread=12.0)
+    d = b.desc()
+    rays = np.concatenate([_random_rays(50000, -15, 15, seed=n), _random_rays(50000, -60, 60, seed=n + 1)])
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    with yart.option("world_bvh", 1):
+        s = yart.DeviceScene(d)
+        assert s.info().world_nodes > 0
+        h, o = s.intersect(rays)
+    assert (o2 >= 0).mean() > 0.025  # 3 % (n = 17) to 32 % (n = 600) of the rays hit
+    _hits_equal(h, o, h2, o2)
+
+
 def test_world_bvh_ties_go_to_the_later_object(dev):
     """Coincident primitives hit at the same t: the linear scan keeps the LAST one (t == t_max is
     accepted); the BVH must pick the same object whatever order it visits them in."""

@@ -82,33 +82,13 @@ def test_world_bvh_4wide_structure(scene):
 
 def test_world_bvh_4wide_structure_on_mixed_synthetic_lists():
     """Random lists of plain, hollow and translated spheres, rects, rotated / translated boxes and
-    triangles, 1 to 600 objects: the 4-wide tree passes its structural check for every list of more
-    than one leaf (a list the SAH keeps in one leaf stays on the linear walk), and a list holding a moving sphere is
-    left to the linear walk (built = 0)."""
-    import numpy as np
+    triangles, 1 to 600 objects (oracle_lib.mixed_list_desc): the 4-wide tree passes its structural
+    check for every list of more than one leaf (a list the SAH keeps in one leaf stays on the linear
+    walk), and a list holding a moving sphere is left to the linear walk (built = 0)."""
     import oracle_lib as O
     from yart import abi
-    rng = np.random.default_rng(31)
     for n in [1, 2, 3, 4, 5, 16, 17, 63, 64, 65, 257, 600]:
-        b = O.DescBuilder()
-        m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
-        for k in range(n):
-            c = tuple(float(x) for x in rng.uniform(-50, 50, 3))
-            kind = k % 6
-            if kind == 0:
-                b.obj(abi.PRIM_SPHERE, m, c + (float(rng.uniform(0.1, 3)),))
-            elif kind == 1:
-                b.obj(abi.PRIM_SPHERE, m, (0.0, 0.0, 0.0, -float(rng.uniform(0.1, 3))), xforms=[(abi.XF_TRANSLATE, c)])
-            elif kind == 2:
-                b.obj(abi.PRIM_XZ_RECT, m, (c[0], c[0] + 4.0, c[2], c[2] + 3.0, c[1]))
-            elif kind == 3:
-                b.obj(abi.PRIM_BOX, m, (0.0, 0.0, 0.0, 2.0, 5.0, 1.0),
-                      xforms=[(abi.XF_TRANSLATE, c), (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))])
-            elif kind == 4:
-                v = rng.uniform(-2, 2, 9) + np.tile(c, 3)
-                b.obj(abi.PRIM_TRIANGLE, m, tuple(float(x) for x in v) + (0.0, 1.0, 0.0) * 3 + (0.0,) * 6)
-            else:
-                b.obj(abi.PRIM_YZ_RECT, m, (c[1], c[1] + 2.0, c[2], c[2] + 2.0, c[0]), xforms=[(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))])
+        b = O.mixed_list_desc(n, seed=31 + n)
         info = yart.world_bvh_build(b.desc())
         assert info["built"] == 0 or info["valid"] == 1, (n, info)
         assert info["built"] == 1 or n <= 4, (n, info)  # a single leaf stays on the linear walk
