@@ -47,6 +47,21 @@ def test_library_reads_no_environment(repo):
         assert not imported & {"getenv", "secure_getenv", "__secure_getenv"}, name
 
 
+def test_rotate_y_uses_the_oracles_sincos(repo):
+    """RotateY's sin / cos (hittable.rs:173-176) are formed on the host: by one glibc sincos call in
+    the device library, as gcc builds the oracle and as LLVM builds the reference (a sin and a cos of
+    one value become sincos on GNU targets). glibc's separate sin differs from sincos by an ulp for
+    some angles (found by test_world_bvh_4wide_mixed_lists_match_linear_scan: 160.037 degrees)."""
+    def imports(so):
+        out = subprocess.run(["nm", "-D", "--undefined-only", str(so)], capture_output=True, text=True,
+                             check=True).stdout
+        return {line.split()[-1].split("@")[0] for line in out.splitlines() if line.strip()}
+    dev = imports(repo / "yet-another-raytracer_amd" / "lib" / "libyart.so")
+    orc = imports(repo / "oracle" / "liboracle.so")
+    assert "sincos" in dev and not dev & {"sin", "cos"}
+    assert "sincos" in orc
+
+
 def test_device_library_loads_without_gpu():
     L = yart.load_device()  # loading must not touch the GPU
     assert L.yart_version().decode().startswith("yart-mi355x")

@@ -117,8 +117,13 @@ DevObject to_dev(const yart_object& o) {
     d.xf_kind[l] = o.xforms[l].kind;
     if (o.xforms[l].kind == YART_XF_ROTATE_Y) {  // RotateY::new (hittable.rs:173-176)
       const double radians = o.xforms[l].v[0] * 3.141592653589793 / 180.0;
-      d.xf[l][0] = std::sin(radians);
-      d.xf[l][1] = std::cos(radians);
+      // One sincos call, as the reference's build makes it (LLVM joins a sin and a cos of the same
+      // value into glibc's sincos on GNU targets) and as gcc builds the oracle: glibc's separate sin
+      // differs from sincos by an ulp for some angles (160.037...°: 0.34141019606902406 vs ...401).
+      double sn, cs;
+      ::sincos(radians, &sn, &cs);
+      d.xf[l][0] = sn;
+      d.xf[l][1] = cs;
     } else if (o.xforms[l].kind == YART_XF_MEDIUM) {  // ConstantMedium::new (hittable.rs:270)
       d.xf[l][0] = -1.0 / o.xforms[l].v[0];
     } else {
