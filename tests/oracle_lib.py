@@ -233,7 +233,7 @@ class DescBuilder:
         return C.pointer(d)
 
 
-def mixed_list_desc(n, seed, spread=50.0):
+def mixed_list_desc(n, seed, spread=50.0, shaded=False):
     """A scene description of n mixed list entries (test infrastructure): plain and hollow
     translated spheres, XZ rects, translated + rotated boxes, triangles and flipped YZ rects at
     random places within +-spread, one Lambertian material. The world BVH's structural and parity
@@ -242,9 +242,17 @@ def mixed_list_desc(n, seed, spread=50.0):
     rng = np.random.default_rng(seed)
     b = DescBuilder()
     m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    mats = [m]
+    if shaded:  # every material kind of the list kernels: checker, metal, glass, emitter
+        mats += [b.material(abi.MAT_LAMBERTIAN, b.texture((0.9, 0.1, 0.1), (0.1, 0.1, 0.9))),
+                 b.material(abi.MAT_METAL, b.texture((0.8, 0.8, 0.6)), fuzz=0.3),
+                 b.material(abi.MAT_DIELECTRIC, b=(1.73759695, 0.313747346, 1.89878101),
+                            c=(0.013188707, 0.0623068142, 155.23629)),
+                 b.material(abi.MAT_DIFFUSE_LIGHT, b.texture((4.0, 4.0, 4.0)))]
     for k in range(n):
         c = tuple(float(x) for x in rng.uniform(-spread, spread, 3))
         kind = k % 6
+        m = mats[int(rng.integers(0, len(mats)))]
         if kind == 0:
             b.obj(abi.PRIM_SPHERE, m, c + (float(rng.uniform(0.1, 3)),))
         elif kind == 1:
@@ -259,4 +267,22 @@ def mixed_list_desc(n, seed, spread=50.0):
             b.obj(abi.PRIM_TRIANGLE, m, tuple(float(x) for x in v) + (0.0, 1.0, 0.0) * 3 + (0.0,) * 6)
         else:
             b.obj(abi.PRIM_YZ_RECT, m, (c[1], c[1] + 2.0, c[2], c[2] + 2.0, c[0]), xforms=[(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))])
+    if shaded:  # rotated spheres, rects and triangles too, and a light list (rect + sphere)
+        for k in range(n // 4):
+            c = tuple(float(x) for x in rng.uniform(-spread, spread, 3))
+            rot = (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))
+            m = mats[int(rng.integers(0, len(mats)))]
+            if k % 3 == 0:
+                b.obj(abi.PRIM_SPHERE, m, c + (float(rng.uniform(0.3, 2)),), xforms=[rot])
+            elif k % 3 == 1:
+                b.obj(abi.PRIM_XY_RECT, m, (c[0], c[0] + 3.0, c[1], c[1] + 2.0, c[2]), xforms=[rot])
+            else:
+                v = rng.uniform(-2, 2, 9) + np.tile(c, 3)
+                b.obj(abi.PRIM_TRIANGLE, m, tuple(float(x) for x in v) + (0.0, 0.0, 1.0) * 3 + (0.0,) * 6,
+                      xforms=[(abi.XF_TRANSLATE, (0.5, 0.0, -0.5)), rot])
+        light = mats[-1]
+        b.obj(abi.PRIM_XZ_RECT, light, (-3.0, 3.0, -3.0, 3.0, spread + 4.0), xforms=[(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))])
+        b.obj(abi.PRIM_XZ_RECT, light, (-3.0, 3.0, -3.0, 3.0, spread + 4.0), light=True)
+        b.obj(abi.PRIM_SPHERE, light, (0.0, -spread - 6.0, 0.0, 2.0))
+        b.obj(abi.PRIM_SPHERE, light, (0.0, -spread - 6.0, 0.0, 2.0), light=True)
     return b

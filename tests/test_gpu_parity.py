@@ -330,6 +330,26 @@ def test_world_bvh_4wide_mixed_lists_match_linear_scan(dev, n):
     _hits_equal(h, o, h2, o2)
 
 
+@pytest.mark.parametrize("world_bvh", [0, 1])
+def test_mixed_shaded_lists_render_like_the_oracle(dev, world_bvh):
+    """Renders of random mixed lists with every list material (Lambertian, checker, fuzzy metal,
+    glass, emitters), RotateY at random angles on spheres, rects, triangles and boxes, Translate,
+    FlipFace, and a rect + sphere light list: the linear list kernel (world_bvh = 0) and the
+    4-wide world BVH (1), bitwise the oracle's frame (the same Philox stream)."""
+    b = O.mixed_list_desc(48, seed=77, spread=8.0, shaded=True)
+    b.background = (0.3, 0.4, 0.5)
+    d = b.desc()
+    W, H, spp = 40, 30, 8
+    cam = yart.make_camera((0.0, 2.0, 30.0), (0.0, 0.0, 0.0), 45.0, W / H, 0.05, 10.0)
+    with yart.option("world_bvh", world_bvh):
+        s = yart.DeviceScene(d)
+        assert (s.info().world_nodes > 0) == (world_bvh == 1)
+        img = s.render(cam, yart.render_params(W, H, spp, 20))
+    ref = O.OracleScene(d).render(cam, yart.render_params(W, H, spp, 20))
+    assert np.isfinite(ref).all() and ref.mean() > 0.0
+    np.testing.assert_array_equal(img, ref)
+
+
 def test_world_bvh_ties_go_to_the_later_object(dev):
     """Coincident primitives hit at the same t: the linear scan keeps the LAST one (t == t_max is
     accepted); the BVH must pick the same object whatever order it visits them in."""
