@@ -573,6 +573,47 @@ def _deep_grid(n=1450):
     return pos, np.ascontiguousarray(np.repeat(nrm, 3, axis=0).reshape(-1, 9))
 
 
+def test_mesh_instances_at_random_angles_match_oracle(dev, repo):
+    """Six instances of the sycee stand-in mesh under RotateY at random angles (and Translate, one
+    under FlipFace), diffuse, metal and glass, with a sphere light: closest hits of 60k rays aimed
+    at the instances and a small render, bitwise the oracle's. The instances' sin / cos come from
+    the host (one sincos each, test_rotate_y_uses_the_oracles_sincos); the walk runs on the
+    rotated local rays."""
+    pos, nrm = yart.load_obj(repo / "assets" / "sycee.obj")
+    b = O.DescBuilder(background=(0.5, 0.6, 0.7))
+    mats = [b.material(abi.MAT_LAMBERTIAN, b.texture((0.7, 0.6, 0.5))),
+            b.material(abi.MAT_METAL, b.texture((0.9, 0.9, 0.8)), fuzz=0.1),
+            b.material(abi.MAT_DIELECTRIC, 0, b=(1.62153902, 0.256287842, 1.64447552),
+                       c=(0.0122241457e6, 0.0595736775e6, 147.468793e6))]
+    li = b.material(abi.MAT_DIFFUSE_LIGHT, b.texture((6.0, 6.0, 6.0)))
+    b.mesh(pos, nrm)
+    rng = np.random.default_rng(91)
+    centres = []
+    for k in range(6):
+        c = (float(rng.uniform(-6, 6)), float(rng.uniform(-1, 1)), float(rng.uniform(-6, 6)))
+        centres.append(c)
+        xf = [(abi.XF_TRANSLATE, c), (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))]
+        if k == 5:
+            xf = [(abi.XF_FLIP_FACE, (0.0, 0.0, 0.0))] + xf
+        b.obj(abi.PRIM_MESH, mats[k % 3], mesh=0, xforms=xf)
+    b.obj(abi.PRIM_SPHERE, li, (0.0, 9.0, 0.0, 2.0))
+    b.obj(abi.PRIM_SPHERE, li, (0.0, 9.0, 0.0, 2.0), light=True)
+    d = b.desc()
+    n = 60000
+    org = rng.uniform(-12, 12, (n, 3))
+    tgt = np.array(centres)[rng.integers(0, 6, n)] + rng.normal(scale=1.0, size=(n, 3))
+    rays = np.column_stack([org, tgt - org, np.full(n, 0.001), np.full(n, np.inf)])
+    s = yart.DeviceScene(d)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, o, h2, o2)
+    W, H, spp = 32, 24, 4
+    cam = yart.make_camera((0.0, 4.0, 18.0), (0.0, 0.0, 0.0), 50.0, W / H, 0.0, 10.0)
+    np.testing.assert_array_equal(s.render(cam, yart.render_params(W, H, spp, 16)),
+                                  O.OracleScene(d).render(cam, yart.render_params(W, H, spp, 16)))
+
+
 def test_deep_mesh_walks_with_the_references_64_slot_stack(dev):
     """A mesh deeper than depth 10 (VERDICT r02 Missing #3): the reference walks it with its
     64-entry stack (qbvh.rs:382-384); here the wavefront trace kernel's 64-slot cooperative walk
