@@ -350,6 +350,43 @@ def test_mixed_shaded_lists_render_like_the_oracle(dev, world_bvh):
     np.testing.assert_array_equal(img, ref)
 
 
+def test_mixed_shaded_lists_with_extended_features_render_like_the_oracle(dev):
+    """The EXT kernel on a random mixed list: the shaded list above plus noise-textured spheres (all
+    five noise types, some under RotateY), an image-textured box and triangle under RotateY, a
+    rotated ConstantMedium box with an isotropic phase function, and moving spheres (which put the
+    shutter-time draw in every camera ray): the frame bitwise the oracle's."""
+    b = O.mixed_list_desc(36, seed=78, spread=8.0, shaded=True)
+    b.background = (0.2, 0.3, 0.4)
+    rng = np.random.default_rng(79)
+    img = rng.integers(0, 256, (16, 24, 3), dtype=np.uint8)
+    imat = b.material(abi.MAT_LAMBERTIAN, b.image_texture(img))
+    for k in range(5):
+        nm = b.material(abi.MAT_LAMBERTIAN, b.noise_texture(k, float(rng.uniform(0.5, 4.0)), seed=80 + k))
+        c = tuple(float(x) for x in rng.uniform(-6, 6, 3))
+        xf = [(abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))] if k % 2 else []
+        b.obj(abi.PRIM_SPHERE, nm, c + (float(rng.uniform(0.8, 2.0)),), xforms=xf)
+    rot = (abi.XF_ROTATE_Y, (float(rng.uniform(-180, 180)), 0.0, 0.0))
+    b.obj(abi.PRIM_BOX, imat, (-1.0, -1.0, -1.0, 1.0, 2.0, 1.5), xforms=[(abi.XF_TRANSLATE, (3.0, 0.0, -2.0)), rot])
+    v = rng.uniform(-3, 3, 9)
+    b.obj(abi.PRIM_TRIANGLE, imat, tuple(float(x) for x in v) + (0.0, 1.0, 0.0) * 3 + (0.0, 0.0, 1.0, 0.0, 0.0, 1.0),
+          xforms=[rot])
+    fog = b.material(abi.MAT_ISOTROPIC, b.texture((0.8, 0.8, 0.9)))
+    b.obj(abi.PRIM_BOX, fog, (-2.0, -2.0, -2.0, 2.0, 2.0, 2.0),
+          xforms=[(abi.XF_MEDIUM, (0.2, 0.0, 0.0)), (abi.XF_TRANSLATE, (-3.0, 1.0, 1.0)), rot])
+    red = b.material(abi.MAT_LAMBERTIAN, b.texture((0.7, 0.3, 0.1)))
+    for k in range(3):
+        c0 = (-4.0 + 4.0 * k, 3.0, 2.0)
+        b.obj(abi.PRIM_MOVING_SPHERE, red, c0 + (c0[0], 3.5 + 0.5 * k, 2.0, 0.0, 1.0, 0.6))
+    d = b.desc()
+    W, H, spp = 40, 30, 8
+    cam = yart.make_camera((0.0, 2.0, 30.0), (0.0, 0.0, 0.0), 45.0, W / H, 0.05, 10.0)
+    s = yart.DeviceScene(d)
+    out = s.render(cam, yart.render_params(W, H, spp, 20))
+    ref = O.OracleScene(d).render(cam, yart.render_params(W, H, spp, 20))
+    assert np.isfinite(ref).all() and ref.mean() > 0.0
+    np.testing.assert_array_equal(out, ref)
+
+
 def test_world_bvh_ties_go_to_the_later_object(dev):
     """Coincident primitives hit at the same t: the linear scan keeps the LAST one (t == t_max is
     accepted); the BVH must pick the same object whatever order it visits them in."""
