@@ -21,5 +21,7 @@ drain, idle = st.mesh_rewalks, st.coop_leaf_rounds
 steps = st.node_visits + st.leaf_visits
 print(f"{scene} {W}x{H}x{spp}: walks {walks}, rounds {rounds} ({rounds / walks:.1f} per walk), quad steps {steps} "
       f"({steps / (16 * rounds):.1%} of quad slots)")
+print(f"  segments {st.segments}, wave walks per 64 segments {64 * walks / st.segments:.2f} (a wave walks each mesh "
+      f"instance a segment's rays may hit)")
 print(f"  rounds with the pool exhausted: {drain} ({drain / rounds:.1%}); their idle quad slots {idle} "
       f"({idle / (16 * rounds):.1%} of all quad slots)")
