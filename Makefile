@@ -32,8 +32,11 @@ $(LIB)/libyart_host.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIB)
 	g++ $(CXXFLAGS) -shared -o $@ $(HOST_SRCS)
 
-$(LIB)/libyart.so: $(DEV_SRCS) $(DEV_HDRS) $(GEN)/cie_xyz.inc $(GEN)/smits.inc
+# build/gen/build_id.h: sha256 of the sources (yart/buildid.py), returned by yart_build_id(); the
+# Python side refuses a libyart.so whose id is not the tree's (a stale prebuilt library)
+$(LIB)/libyart.so: $(DEV_SRCS) $(DEV_HDRS) $(GEN)/cie_xyz.inc $(GEN)/smits.inc $(ROOT)/Makefile
 	@mkdir -p $(LIB)
+	python3 $(PKG)/yart/buildid.py --header $(GEN)/build_id.h
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(DEV_SRCS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(BIN)/yart: $(PKG)/host/main.cpp $(LIB)/libyart.so $(LIB)/libyart_host.so
@@ -48,5 +51,6 @@ clean:
 # A/B builds for tools/ab.py: make variant NAME=x DEFS="-DYART_FOO"
 variant: $(GEN)/cie_xyz.inc $(GEN)/smits.inc
 	@mkdir -p $(LIB)/variants
+	python3 $(PKG)/yart/buildid.py --header $(GEN)/build_id.h
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIB)/variants/libyart_$(NAME).so $(DEV_SRCS) -L/opt/rocm/lib -lrccl
 .PHONY: variant

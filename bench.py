@@ -134,9 +134,11 @@ def kernels_sha256():
     return hashlib.sha256((ROOT / "yet-another-raytracer_amd" / "csrc" / "kernels.hip").read_bytes()).hexdigest()
 
 
-def pmc_snapshot():
+def pmc_snapshot(build_id):
     """The committed rocprofv3 PMC summary of the render kernel (tools/profile.sh +
-    tools/summarize_profiles.py), if it was taken on the current kernel source."""
+    tools/summarize_profiles.py), if it was taken on the library this run loaded (its build id,
+    the sha256 of every libyart.so source) — or, for a snapshot older than build ids, on the
+    current kernels.hip."""
     p = ROOT / "profiles" / "pmc_render_cornell.json"
     if not p.exists():
         return {}, "no profile"
@@ -144,9 +146,25 @@ def pmc_snapshot():
         pmc = json.loads(p.read_text())
     except Exception:
         return {}, "unreadable profile"
+    if "build_id" in pmc:
+        if pmc["build_id"] != build_id:
+            return {}, "stale: profiles/pmc_render_cornell.json was taken on another libyart.so build"
+        return pmc, "profiles/pmc_render_cornell.json (rocprofv3 --pmc snapshot of this libyart.so build)"
     if pmc.get("kernels_sha256") != kernels_sha256():
         return {}, "stale: profiles/pmc_render_cornell.json was taken on another kernels.hip"
     return pmc, "profiles/pmc_render_cornell.json (rocprofv3 --pmc snapshot of this kernel source)"
+
+
+def device_balance(render_ms, gather_ms):
+    """Per-device render / gather times of an N-GPU frame (ms, one frame): the fields that say,
+    when a scaling run falls short, whether load imbalance or the gather is the cause (VERDICT r04
+    item 5). gather_ms[d] is device d's own gather interval (it includes waiting for the others)."""
+    n = len(render_ms)
+    mean = sum(render_ms) / n if n else 0.0
+    return {"per_device_render_ms": [round(x, 3) for x in render_ms],
+            "per_device_gather_ms": [round(x, 3) for x in gather_ms] if gather_ms is not None else None,
+            "render_max_over_mean": round(max(render_ms) / mean, 4) if mean > 0 else None,
+            "slowest_device": int(max(range(n), key=lambda d: render_ms[d])) if n else None}
 
 
 def valu_issue(pmc):
@@ -238,7 +256,8 @@ def main():
     frames = [torch.zeros((H, W, 3), dtype=torch.float64, device=dev) for _ in range(S)]  # rank 0: assembled
     rgbas = [torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) for _ in range(S)]
     frame = frames[0]
-    L = yart.load_device()
+    L = yart.load_device()  # refuses a libyart.so not built from this tree (yart.StaleLibraryError)
+    build_id = L.yart_build_id().decode()
 
     # N > 1, one process per GPU: the data-plane collective, chosen ONCE and identically on every rank
     collective, comm, gather, nccl_group = None, None, None, None
@@ -274,6 +293,7 @@ def main():
                     collective = "gather (torch.distributed nccl, fallback)"
 
     coll_done = [None]  # the previous step's collective (ranks, N > 1): the next one waits for it
+    gather_evs = []     # ranks, N > 1: this rank's (start, end) timing events around each step's gather
     last = {}           # the latest step's stage events (single / ranks): where a stalled frame stands
 
     def mark(key, st):
@@ -314,6 +334,8 @@ def main():
                 mark("render", st)
                 if coll_done[0] is not None:
                     st.wait_event(coll_done[0])
+                g0 = torch.cuda.Event(enable_timing=True)
+                g0.record(st)
                 if comm is not None:
                     comm.gather_frame_async(packed.data_ptr(), W, H, frame.data_ptr(), st.cuda_stream)
                 elif rehearse:
@@ -324,6 +346,9 @@ def main():
                 else:
                     gather(packed, frame, dist, group=nccl_group)
                 mark("gather", st)
+                g1 = torch.cuda.Event(enable_timing=True)
+                g1.record(st)
+                gather_evs.append((g0, g1))
                 coll_done[0] = last["gather"]
             if rank == 0:
                 rc = L.yart_finalize_rgba8_async(local, yart.C.c_void_p(frame.data_ptr()), W, H, spp,
@@ -383,11 +408,24 @@ def main():
     # (a launch's events bracket its wait for the slots the previous frame still holds), so the
     # kernel's own duration is taken from 3 frames on one stream right after the timed region.
     if S > 1:
+        gather_evs.clear()
         with wd.stage("kernel-time frames (one stream)", frames_deadline(3), where):
             for i in range(3):
                 step(i, streams=streams[:1])
             sync_all()
         render_ms, accum_ms, nfr = drain_timing()
+    # per-device balance of the same frames (N > 1): render-kernel and own-gather time per device
+    balance = None
+    if mode == "multi":
+        dr, dg, dn = multi.device_timing()
+        balance = device_balance([x / max(1, dn) for x in dr], [x / max(1, dn) for x in dg])
+    elif mode == "ranks":
+        my_gather = (sum(a.elapsed_time(b) for a, b in gather_evs) / len(gather_evs)) if gather_evs else 0.0
+        with wd.stage("per-rank timings (all_gather)", BASE_DEADLINE_S):
+            mine = torch.tensor([render_ms / max(1, nfr), my_gather], dtype=torch.float64)
+            every = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(every, mine)
+        balance = device_balance([float(t[0]) for t in every], [float(t[1]) for t in every])
     kern_ms = render_ms / max(1, nfr)      # k_render average launch duration (one stream; multi: slowest GPU)
     accum_ms = accum_ms / max(1, nfr)      # k_accumulate (chunked path); multi: the root's gather + unpack
     if mode == "multi":
@@ -417,7 +455,7 @@ def main():
         flops = (st.samples * FLOPS["sample"] + st.segments * FLOPS["segment"] + st.prim_tests * FLOPS["prim"] +
                  st.node_visits * FLOPS["node"] + st.leaf_tris * FLOPS["leaf_tri"] + st.light_tests * FLOPS["light"])
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        pmc, pmc_source = pmc_snapshot()
+        pmc, pmc_source = pmc_snapshot(build_id)
         traffic = pmc.get("hbm_bytes_per_launch") if world == 1 else None
         chunked = mode == "multi" or (accum_ms or 0) > 0
         roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -447,6 +485,8 @@ def main():
                                                if world == 1 and pmc.get("SQ_INSTS_VALU") and st.segments else None)}
         if mode == "multi":
             roofline["gather_ms"] = round(gather_ms, 3)
+        if balance is not None:
+            roofline.update(balance)
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         with wd.stage("cpu baseline (oracle on the host cores)", 900.0):
             cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
@@ -464,8 +504,11 @@ def main():
                        "launch": {"single": "one process, one GPU", "multi": "one process, N GPUs",
                                   "ranks": "one process per GPU (torch.distributed.run)"}[mode],
                        "streams": S, "prep_frames": prep,
-                       "collective": collective, "frame_check": frame_check, "seed": yart.DEFAULT_SEED},
+                       "collective": collective, "frame_check": frame_check, "seed": yart.DEFAULT_SEED,
+                       "build_id": build_id},
             "roofline": roofline, "cpu_baseline": cpu,
+            # N > 1: per-device render / own-gather ms and render max / mean (also in roofline)
+            "device_balance": balance,
         }
         print(json.dumps(line), flush=True)
     with wd.stage("teardown (communicators, process group)", BASE_DEADLINE_S):

@@ -286,3 +286,45 @@ def mixed_list_desc(n, seed, spread=50.0, shaded=False):
         b.obj(abi.PRIM_SPHERE, light, (0.0, -spread - 6.0, 0.0, 2.0))
         b.obj(abi.PRIM_SPHERE, light, (0.0, -spread - 6.0, 0.0, 2.0), light=True)
     return b
+
+
+def big_sphere_desc(n, seed, clustered):
+    """A list of n plain spheres built straight into the C arrays (test infrastructure; n up to
+    millions): uniform in a 2000-unit cube, or clustered — 64 centres, each with its own spread
+    from 1e-6 to 10 units, radii from 1e-7 to 1 — the kind of list whose SAH tree runs deep
+    (the 4-wide collapse then exceeded the walk's stack and the BVH was dropped).
+    Returns (POINTER(SceneDesc), keep-alive tuple)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    b = DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    objs = (abi.Object * n)()
+    raw = np.frombuffer(objs, dtype=np.uint8).reshape(n, C.sizeof(abi.Object))
+    u32 = raw[:, :16].view(np.uint32)
+    u32[:, 0] = abi.PRIM_SPHERE
+    u32[:, 1] = m
+    if clustered:
+        centres = rng.uniform(-1000, 1000, (64, 3))
+        spread = 10.0 ** rng.uniform(-6, 1, 64)
+        k = rng.integers(0, 64, n)
+        c = centres[k] + rng.normal(0, 1, (n, 3)) * spread[k][:, None]
+        r = 10.0 ** rng.uniform(-7, 0, n)
+    else:
+        c = rng.uniform(-1000, 1000, (n, 3))
+        r = rng.uniform(0.1, 1.0, n)
+    off = abi.Object.p.offset
+    p = np.zeros((n, 4))
+    p[:, :3] = c
+    p[:, 3] = r
+    raw[:, off:off + 32] = p.view(np.uint8)
+    d = abi.SceneDesc()
+    d.abi_version = abi.ABI_VERSION
+    d.n_objects, d.n_lights, d.n_materials, d.n_textures, d.n_meshes = n, 0, 1, 1, 0
+    mats = (abi.Material * 1)(*b.materials)
+    texs = (abi.Texture * 1)(*b.textures)
+    d.objects = C.cast(objs, C.POINTER(abi.Object))
+    d.materials = C.cast(mats, C.POINTER(abi.Material))
+    d.textures = C.cast(texs, C.POINTER(abi.Texture))
+    d.background = (C.c_double * 3)(0.5, 0.6, 0.7)
+    keep = (objs, mats, texs, b, d)
+    return C.pointer(d), keep

@@ -132,3 +132,45 @@ def test_bench_stalled_first_stage_exits_nonzero_naming_it():
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1 and lines[0]["value"] is None
     assert lines[0]["stage"].startswith("process group init") and "deadline" in lines[0]["error"]
+
+
+def test_device_balance_fields():
+    """an N-GPU line says which device was slowest and how long each waited in
+    the gather, so a scaling shortfall can be told apart as imbalance or gather cost."""
+    sys.path.insert(0, str(ROOT))
+    import importlib
+    bench = importlib.import_module("bench")
+    b = bench.device_balance([4.10, 4.20, 4.00, 4.30], [0.40, 0.30, 0.50, 0.20])
+    assert b["per_device_render_ms"] == [4.1, 4.2, 4.0, 4.3]
+    assert b["per_device_gather_ms"] == [0.4, 0.3, 0.5, 0.2]
+    assert b["render_max_over_mean"] == pytest.approx(4.30 / 4.15, rel=1e-3)
+    assert b["slowest_device"] == 3
+
+
+def test_rehearsal_line_carries_the_per_device_fields():
+    """The committed N = 2 rehearsal of bench.py's per-rank path (profiles/r05_rehearse_n2.log,
+    YART_BENCH_SAME_DEVICE=1: both ranks on one GPU, gloo gather) carries the per-device fields."""
+    logs = sorted(PROF.glob("r0[5-9]*_rehearse_n2.log"))
+    if not logs:
+        pytest.skip("no r05+ rehearsal log")
+    lines = [json.loads(l) for l in logs[-1].read_text().splitlines() if l.startswith("{")]
+    assert lines, logs[-1]
+    b = lines[-1]
+    assert b["n_gpus"] == 2
+    bal = b["device_balance"]
+    assert len(bal["per_device_render_ms"]) == 2 and len(bal["per_device_gather_ms"]) == 2
+    assert bal["render_max_over_mean"] >= 1.0
+    assert b["roofline"]["per_device_render_ms"] == bal["per_device_render_ms"]
+    assert len(b["config"]["build_id"]) == 64
+
+
+def test_bench_line_build_id_matches_the_pmc_snapshot():
+    """the newest bench line names the library build it timed, and the PMC
+    snapshot it took traffic from belongs to the same build."""
+    _, b = _bench_line()
+    bid = b["config"].get("build_id")
+    if bid is None:
+        pytest.skip("bench line older than build ids")
+    pmc = json.loads((PROF / "pmc_render_cornell.json").read_text())
+    if b["roofline"]["traffic"] is not None:
+        assert pmc.get("build_id") == bid

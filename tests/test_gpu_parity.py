@@ -330,6 +330,28 @@ def test_world_bvh_4wide_mixed_lists_match_linear_scan(dev, n):
     _hits_equal(h, o, h2, o2)
 
 
+def test_world_bvh_of_a_large_clustered_list_matches_linear_scan(dev):
+    """65,536 clustered spheres (oracle_lib.big_sphere_desc), a list whose SAH tree
+    the area collapse made too deep for the walk's stack — the scene used to lose its BVH. Now it
+    keeps one (the median-split fallback of world_bvh.cpp), and closest hits of rays aimed at the
+    spheres are bitwise the oracle's linear HittableList scan."""
+    d, keep = O.big_sphere_desc(1 << 16, seed=7, clustered=True)
+    rng = np.random.default_rng(5)
+    objs = np.frombuffer(keep[0], dtype=np.uint8).reshape(1 << 16, C.sizeof(abi.Object))
+    cent = objs[:, abi.Object.p.offset:abi.Object.p.offset + 24].copy().view(np.float64)
+    n = 4000
+    o = rng.uniform(-1100, 1100, (n, 3))
+    tgt = cent[rng.integers(0, len(cent), n)] + rng.normal(0, 1e-3, (n, 3))
+    rays = np.concatenate([o, tgt - o, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+    s = yart.DeviceScene(d)
+    assert s.info().world_nodes > 0
+    h, ob = s.intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, ob, h2, o2)
+    del keep
+
+
 @pytest.mark.parametrize("world_bvh", [0, 1])
 def test_mixed_shaded_lists_render_like_the_oracle(dev, world_bvh):
     """Renders of random mixed lists with every list material (Lambertian, checker, fuzzy metal,

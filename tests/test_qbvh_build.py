@@ -98,3 +98,18 @@ def test_world_bvh_4wide_structure_on_mixed_synthetic_lists():
         b.obj(abi.PRIM_SPHERE, m, (float(k), 0.0, 0.0, 0.4))
     b.obj(abi.PRIM_MOVING_SPHERE, m, (0.0, 1.0, 0.0, 1.0, 1.0, 0.0, 0.0, 1.0, 0.3))
     assert yart.world_bvh_build(b.desc())["built"] == 0
+
+
+@pytest.mark.parametrize("n,clustered", [(1 << 16, True), (1 << 18, False), (1 << 20, True)])
+def test_world_bvh_large_and_clustered_lists_keep_their_bvh(n, clustered):
+    """the 4-wide collapse by largest area can run deeper than the walk's 32-slot stack
+    (3 depth4 + 1 <= 32) for a deep binary tree, and scene creation then fell back to the O(n)
+    linear list walk with no sign but world_nodes = 0 (every case here was built = 0 before the
+    fix). The builder now collapses two binary levels per node, then rebuilds by median splits with
+    larger leaves, before giving up: a million clustered spheres keep a valid tree."""
+    import oracle_lib as O
+    d, keep = O.big_sphere_desc(n, seed=7, clustered=clustered)
+    info = yart.world_bvh_build(d)
+    assert info["built"] == 1 and info["valid"] == 1, info
+    assert 3 * info["depth4"] + 1 <= 32
+    del keep

@@ -64,6 +64,11 @@ def main():
     # which kernel source the counters belong to: bench.py reports the traffic only while
     # csrc/kernels.hip still hashes to this value
     summary["kernels_sha256"] = kernels_sha256()
+    # and the library's build id (the sha256 of every source libyart.so is built from; the profiled
+    # process refused to load a library whose id was not the tree's, yart/buildid.py)
+    sys.path.insert(0, str(ROOT / "yet-another-raytracer_amd"))
+    from yart import buildid
+    summary["build_id"] = buildid.build_id()
     (PROF / f"{tag}_pmc.json").write_text(json.dumps(summary, indent=1) + "\n")
     if "cornell" in tag or tag.endswith("_render"):
         (PROF / "pmc_render_cornell.json").write_text(json.dumps(summary, indent=1) + "\n")

@@ -17,6 +17,7 @@
 
 #include "../../include/yart.h"
 #include "../host/camera_impl.h"
+#include "build_id.h"  // generated (Makefile): YART_BUILD_ID
 #include "bvh_build.h"
 #include "kernels.h"
 #include "scene_impl.h"
@@ -117,9 +118,10 @@ DevObject to_dev(const yart_object& o) {
     d.xf_kind[l] = o.xforms[l].kind;
     if (o.xforms[l].kind == YART_XF_ROTATE_Y) {  // RotateY::new (hittable.rs:173-176)
       const double radians = o.xforms[l].v[0] * 3.141592653589793 / 180.0;
-      // One sincos call, as the reference's build makes it (LLVM joins a sin and a cos of the same
-      // value into glibc's sincos on GNU targets) and as gcc builds the oracle: glibc's separate sin
-      // differs from sincos by an ulp for some angles (160.037...°: 0.34141019606902406 vs ...401).
+      // One sincos call, as gcc builds the oracle (it joins the sin and cos of one value into glibc's
+      // sincos): glibc's separate sin differs from sincos by an ulp for some angles (160.037...°:
+      // 0.34141019606902406 vs ...401). This matches the oracle; whether the reference's rustc build
+      // calls sincos or sin and cos is not pinned (ulp-level parity at such angles unpinned).
       double sn, cs;
       ::sincos(radians, &sn, &cs);
       d.xf[l][0] = sn;
@@ -154,6 +156,7 @@ yart_scene::~yart_scene() {
 extern "C" {
 
 const char* yart_version(void) { return "yart-mi355x 0.1 (gfx950, f64 megakernel, ABI 1)"; }
+const char* yart_build_id(void) { return YART_BUILD_ID; }  // build/gen/build_id.h (Makefile)
 const char* yart_last_error(void) { return g_err.c_str(); }
 
 int yart_device_count(int* out) {

@@ -149,6 +149,10 @@ struct MultiSlot {
   size_t recv_bytes = 0;
   // devices[0]: the root's gather + unpack interval of each frame not yet read (timing)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_events;
+  // per device: its ncclGather's interval (from its launch, after its render and the previous
+  // submission's gather, to its end) for each frame not yet read — the per-device balance of the
+  // first N-GPU runs (which device waited in the gather for which)
+  std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> dev_gather_events;
   uint64_t last_use = 0;              // submission number of its latest frame (eviction order)
 };
 
@@ -166,7 +170,12 @@ struct yart_multi {
   double* frame = nullptr;                         // devices[0]: yart_render_multi's frame
   size_t frame_bytes = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gather_pool;  // devices[0]: recycled timing pairs
+  std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> dev_pool;  // per device: recycled timing pairs
   double render_ms = 0.0, gather_ms = 0.0;  // yart_render_multi's last frame
+  // per device, summed over the frames of the latest timing read (yart_multi_frame_timing or
+  // yart_render_multi): render-kernel time and its own gather time (yart_multi_device_timing)
+  std::vector<double> dev_render_ms, dev_gather_ms;
+  uint32_t dev_frames = 0;
   // Drains a slot's streams and frees what it holds (the destructor; eviction of the least recently
   // used slot when a new caller stream would exceed kMaxSlots, so a caller that makes a stream per
   // frame does not grow device memory without bound — ADVICE r03).
@@ -181,6 +190,8 @@ struct yart_multi {
       if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
       if ((size_t)d < s.rendered.size() && s.rendered[(size_t)d]) (void)hipEventDestroy(s.rendered[(size_t)d]);
       if ((size_t)d < s.streams.size() && s.streams[(size_t)d]) (void)hipStreamDestroy(s.streams[(size_t)d]);
+      if ((size_t)d < s.dev_gather_events.size() && (size_t)d < dev_pool.size())
+        for (auto& e : s.dev_gather_events[(size_t)d]) dev_pool[(size_t)d].push_back(e);  // unread: dropped
       if (d == 0) {
         for (auto& e : s.gather_events) gather_pool.push_back(e);  // unread timings are dropped
         s.gather_events.clear();
@@ -195,6 +206,8 @@ struct yart_multi {
     for (auto& kv : slots) release_slot(*kv.second);
     for (int d = 0; d < n && d < (int)devices.size(); ++d) {
       (void)hipSetDevice(devices[(size_t)d]);
+      if ((size_t)d < dev_pool.size())
+        for (auto& e : dev_pool[(size_t)d]) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
       if (d == 0) {
         for (auto& e : gather_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
         if (frame) (void)hipFree(frame);
@@ -235,6 +248,7 @@ int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
     s->packed_bytes.assign((size_t)m->n, 0);
     s->gathered.assign((size_t)m->n, nullptr);
     s->rendered.assign((size_t)m->n, nullptr);
+    s->dev_gather_events.assign((size_t)m->n, {});
     for (int d = 0; d < m->n; ++d) {
       HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
       HIP_TRY(hipStreamCreateWithFlags(&s->streams[(size_t)d], hipStreamNonBlocking), "hipStreamCreate");
@@ -252,10 +266,11 @@ int multi_slot(yart_multi* m, hipStream_t caller, MultiSlot** out) {
   return YART_OK;
 }
 
-int gather_event_pair(yart_multi* m, std::pair<hipEvent_t, hipEvent_t>& out) {  // on devices[0]
-  if (!m->gather_pool.empty()) {
-    out = m->gather_pool.back();
-    m->gather_pool.pop_back();
+// A pair of timing events from `pool` (recycled) or new ones, on the current device.
+int event_pair(std::vector<std::pair<hipEvent_t, hipEvent_t>>& pool, std::pair<hipEvent_t, hipEvent_t>& out) {
+  if (!pool.empty()) {
+    out = pool.back();
+    pool.pop_back();
     return YART_OK;
   }
   HIP_TRY(hipEventCreate(&out.first), "hipEventCreate");
@@ -278,6 +293,9 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   RestoreDevice restore;
   MultiSlot* S = nullptr;
   if (int rc = multi_slot(m, caller, &S)) return rc;
+  // the latest submission from here on, even one that fails partway (yart_multi_query then
+  // describes it, not an older frame whose slot events this one is about to re-record)
+  m->latest = S;
   // 1. renders, one per device, each straight into its packed shard. A wavefront (mesh) frame keeps
   // the host in its launch loop until the frame's last iterations are queued, so those devices are
   // driven from a host thread each, all at once.
@@ -341,15 +359,19 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
     S->recv_bytes = pk_bytes * (size_t)n;
   }
   std::pair<hipEvent_t, hipEvent_t> gev;
-  if (int rc = gather_event_pair(m, gev)) return rc;
+  if (int rc = event_pair(m->gather_pool, gev)) return rc;
   S->gather_events.push_back(gev);
   // 3. ONE gather to devices[0], each device's part right behind its render; in submission order
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> dev_ev((size_t)n);
   for (int d = 0; d < n; ++d) {
     const size_t di = (size_t)d;
     HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
     if (m->last_gather[di] && m->last_gather[di] != S->gathered[di])
       HIP_TRY(hipStreamWaitEvent(S->streams[di], m->last_gather[di], 0), "hipStreamWaitEvent");
     if (d == 0) HIP_TRY(hipEventRecord(gev.first, S->streams[0]), "hipEventRecord");
+    if (int rc = event_pair(m->dev_pool[di], dev_ev[di])) return rc;
+    S->dev_gather_events[di].push_back(dev_ev[di]);
+    HIP_TRY(hipEventRecord(dev_ev[di].first, S->streams[di]), "hipEventRecord");
   }
   NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
   for (int d = 0; d < n; ++d) {
@@ -363,6 +385,7 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   for (int d = 0; d < n; ++d) {
     const size_t di = (size_t)d;
     HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
+    HIP_TRY(hipEventRecord(dev_ev[di].second, S->streams[di]), "hipEventRecord");
     HIP_TRY(hipEventRecord(S->gathered[di], S->streams[di]), "hipEventRecord");
     m->last_gather[di] = S->gathered[di];
   }
@@ -374,20 +397,22 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   HIP_TRY(hipEventRecord(gev.second, S->streams[0]), "hipEventRecord");
   HIP_TRY(hipEventRecord(S->done, S->streams[0]), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(caller, S->done, 0), "hipStreamWaitEvent");
-  m->latest = S;
   return YART_OK;
 }
 
 // Summed kernel times of the frames submitted since the last read, over every slot or one
 // (their streams idle by then): render = the slowest device's summed k_render time,
 // gather = the root's gather + unpack intervals, which include the root's wait for the slowest
-// device's render to finish.
+// device's render to finish. Per device (m->dev_*): its summed render time and the summed
+// intervals of its own ncclGather.
 int multi_timing(yart_multi* m, MultiSlot* only, double* render_ms, double* gather_ms, uint32_t* frames) {
   RestoreDevice restore;
   double worst = 0.0;
   uint32_t nf = 0;
+  m->dev_render_ms.assign((size_t)m->n, 0.0);
+  m->dev_gather_ms.assign((size_t)m->n, 0.0);
   for (int d = 0; d < m->n; ++d) {
-    double r = 0.0;
+    double r = 0.0, dg = 0.0;
     for (auto& kv : m->slots) {
       if (only && kv.second.get() != only) continue;
       double rr = 0.0, acc = 0.0;
@@ -395,9 +420,20 @@ int multi_timing(yart_multi* m, MultiSlot* only, double* render_ms, double* gath
       if (int rc = yart_frame_timing(m->scenes[(size_t)d], kv.second->streams[(size_t)d], &rr, &acc, &f)) return rc;
       r += rr;
       if (d == 0) nf += f;
+      HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
+      for (auto& e : kv.second->dev_gather_events[(size_t)d]) {
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second), "hipEventElapsedTime");
+        dg += ms;
+        m->dev_pool[(size_t)d].push_back(e);
+      }
+      kv.second->dev_gather_events[(size_t)d].clear();
     }
+    m->dev_render_ms[(size_t)d] = r;
+    m->dev_gather_ms[(size_t)d] = dg;
     if (r > worst) worst = r;
   }
+  m->dev_frames = nf;
   HIP_TRY(hipSetDevice(m->devices[0]), "hipSetDevice");
   double g = 0.0;
   for (auto& kv : m->slots) {
@@ -433,6 +469,7 @@ int yart_multi_create(int n, const int* devices, const yart_scene_desc* desc, ya
   m->n = n;
   m->devices.assign(devices, devices + n);
   m->last_gather.assign((size_t)n, nullptr);
+  m->dev_pool.assign((size_t)n, {});
   RestoreDevice restore;
   for (int d = 0; d < n; ++d) {  // the scene is uploaded once per device, here
     yart_scene* s = nullptr;
@@ -516,6 +553,18 @@ int yart_multi_last_timing(const yart_multi* m, double* render_ms, double* gathe
   if (!m || !render_ms || !gather_ms) return fail(YART_ERR_INVALID, "null argument");
   *render_ms = m->render_ms;
   *gather_ms = m->gather_ms;
+  return ok();
+}
+
+int yart_multi_device_timing(yart_multi* m, int n, double* render_ms, double* gather_ms, uint32_t* frames) {
+  if (!m || !render_ms || !gather_ms || !frames) return fail(YART_ERR_INVALID, "null argument");
+  if (n != m->n) return fail(YART_ERR_INVALID, "n must be the multi's device count");
+  std::lock_guard<std::mutex> lk(m->mu);
+  for (int d = 0; d < n; ++d) {
+    render_ms[d] = (size_t)d < m->dev_render_ms.size() ? m->dev_render_ms[(size_t)d] : 0.0;
+    gather_ms[d] = (size_t)d < m->dev_gather_ms.size() ? m->dev_gather_ms[(size_t)d] : 0.0;
+  }
+  *frames = m->dev_frames;
   return ok();
 }
 

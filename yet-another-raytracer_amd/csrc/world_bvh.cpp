@@ -96,6 +96,7 @@ double half_area(const double lo[3], const double hi[3]) {
 struct SahParams {
   size_t max_leaf = 4;
   double node_cost = 0.7;  // one DevWorldNode visit (two f32 box tests) vs one primitive test
+  size_t median_leaf = 2;  // the median splits' leaf size (larger only to bound a huge list's depth)
 };
 size_t sah_split(std::vector<Item>& items, size_t begin, size_t end, const double nlo[3], const double nhi[3],
                  const SahParams& prm) {
@@ -152,7 +153,7 @@ void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, ui
       return;
     }
   }
-  if (cut == 0 && end - begin <= 2) {
+  if (cut == 0 && end - begin <= prm.median_leaf) {
     n.count = (uint32_t)(end - begin);
     n.first = (uint32_t)out.objs.size();
     std::vector<uint32_t> ids;
@@ -183,51 +184,17 @@ void build(std::vector<Item>& items, size_t begin, size_t end, uint32_t node, ui
   build(items, mid, end, left + 1, level + 1, out, sah, prm);
 }
 
-}  // namespace
-
-bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah) {
-  out = BuiltWorld{};
-  if (objs.empty()) return false;
-  std::vector<Item> items(objs.size());
-  for (size_t i = 0; i < objs.size(); ++i) {
-    if (!world_bounds(objs[i], items[i].lo, items[i].hi)) return false;
-    for (int k = 0; k < 3; ++k) items[i].c[k] = 0.5 * (items[i].lo[k] + items[i].hi[k]);
-    items[i].idx = (uint32_t)i;
-  }
-  const SahParams prm;  // node cost and leaf size from the r02 sweep (profiles/r02g_world_sah_sweep.txt)
-  out.nodes.reserve(2 * objs.size());
-  out.nodes.emplace_back();
-  build(items, 0, items.size(), 0, 0, out, sah, prm);
-  // the device walk pushes at most one entry per level into its kStackSlots-deep stack
-  if (sah && out.depth >= (uint32_t)kStackSlots) return build_world_bvh(objs, out, false);
-  // Leaves whose objects are all plain spheres (no wrapper) get kWorldLeafSpheres: the walk reads
-  // their centre and radius from the compact per-slot records instead of the object records.
-  out.sph.assign(4 * out.objs.size(), 0.0);
-  for (size_t j = 0; j < out.objs.size(); ++j) {
-    const DevObject& o = objs[out.objs[j]];
-    if (o.kind == YART_PRIM_SPHERE && o.n_xf == 0)
-      for (int k = 0; k < 4; ++k) out.sph[4 * j + k] = o.p[k];
-  }
-  for (DevWorldNode& n : out.nodes) {
-    if (n.count == 0) continue;
-    bool all = true;
-    for (uint32_t k = 0; k < n.count; ++k) {
-      const DevObject& o = objs[out.objs[n.first + k]];
-      all = all && o.kind == YART_PRIM_SPHERE && o.n_xf == 0;
-    }
-    n.pad[0] = all ? kWorldLeafSpheres : 0u;
-  }
-  // Each leaf's handle (pad[1]): what the walk needs to take the node without reading its record
-  // (the parent's child-box test reads the handle with the box, and the stack holds handles).
-  for (DevWorldNode& n : out.nodes) {
-    if (n.count > kWorldHandleMaxCount || n.first >= kWorldHandleFirstMask) return false;  // the list walk then
-    n.pad[1] = (n.count << 28) | ((n.pad[0] & kWorldLeafSpheres) ? (1u << 27) : 0u) | n.first;
-  }
-  if (out.nodes[0].count != 0) return false;  // a single leaf: the list walk
-  // Collapse into the 4-wide tree: a 4-wide node takes a binary inner node's two children and, while
-  // it has fewer than four, replaces the inner one of largest box area by its own two children.
-  // Children keep the binary nodes' boxes (already rounded outward), so every box test is the one
-  // the binary walk made, and the walk's answer (min t, ties to the later object) is unchanged.
+// Collapse the binary tree into the 4-wide tree the device walks (out.nodes4, out.depth4). A 4-wide
+// node takes a binary inner node's two children and, while it has fewer than four,
+//  * by area (the default): replaces the inner one of largest box area by its own two children —
+//    the best-shaped nodes, but a path may advance only one binary level per 4-wide level;
+//  * two levels: replaces every inner child by its two children once, so each 4-wide level spans
+//    two binary levels and depth4 = ceil(binary depth / 2) (the area rule made a deep
+//    binary tree's 4-wide depth exceed the walk's stack, and the scene silently lost its BVH).
+// Children keep the binary nodes' boxes (already rounded outward), so every box test is the one
+// the binary walk made, and the walk's answer (min t, ties to the later object) is unchanged.
+// Returns whether the walk's stack holds the tree: at most three entries per 4-wide level pushed.
+bool collapse4(BuiltWorld& out, bool two_level) {
   out.nodes4.clear();
   out.depth4 = 0;
   struct Job { uint32_t bin, slot, level; };
@@ -242,13 +209,22 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     const Job j = jobs.back();
     jobs.pop_back();
     out.depth4 = std::max(out.depth4, j.level);
+    if (3 * out.depth4 + 1 > (uint32_t)kStackSlots) return false;
     std::vector<uint32_t> kids{out.nodes[j.bin].first, out.nodes[j.bin].first + 1};
+    if (two_level) {
+      std::vector<uint32_t> next;
+      for (uint32_t b : kids) {
+        if (out.nodes[b].count == 0) { next.push_back(out.nodes[b].first); next.push_back(out.nodes[b].first + 1); }
+        else next.push_back(b);
+      }
+      kids.swap(next);
+    }
     while (kids.size() < 4) {
       int pick = -1;
       double most = -1.0;
       for (int k = 0; k < (int)kids.size(); ++k)
         if (out.nodes[kids[k]].count == 0 && area(kids[k]) > most) { most = area(kids[k]); pick = k; }
-      if (pick < 0) break;
+      if (pick < 0 || two_level) break;
       const uint32_t b = kids[pick];
       kids[pick] = out.nodes[b].first;
       kids.insert(kids.begin() + pick + 1, out.nodes[b].first + 1);
@@ -276,9 +252,67 @@ bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool s
     }
     out.nodes4[j.slot] = q;
   }
-  // the device walk pushes at most three entries per 4-wide level into its kStackSlots-deep stack
-  return out.depth < (uint32_t)kStackSlots && 3 * out.depth4 + 1 <= (uint32_t)kStackSlots;
+  return 3 * out.depth4 + 1 <= (uint32_t)kStackSlots;
 }
+
+// The binary tree (SAH near the root, median splits below) and its 4-wide collapse; a tree the walk's
+// stack cannot hold is collapsed two levels per node, then rebuilt by median splits with leaves of
+// up to 2, 4, 8, 15 objects (depth ~ log2(n / leaf)), before the list walk is the answer.
+bool build_world_bvh_with(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah, size_t median_leaf);
+
+}  // namespace
+
+bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah) {
+  return build_world_bvh_with(objs, out, sah, 2);
+}
+
+namespace {
+
+bool build_world_bvh_with(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah, size_t median_leaf) {
+  out = BuiltWorld{};
+  if (objs.empty()) return false;
+  std::vector<Item> items(objs.size());
+  for (size_t i = 0; i < objs.size(); ++i) {
+    if (!world_bounds(objs[i], items[i].lo, items[i].hi)) return false;
+    for (int k = 0; k < 3; ++k) items[i].c[k] = 0.5 * (items[i].lo[k] + items[i].hi[k]);
+    items[i].idx = (uint32_t)i;
+  }
+  SahParams prm;  // node cost and leaf size from the r02 sweep (profiles/r02g_world_sah_sweep.txt)
+  prm.median_leaf = median_leaf;
+  out.nodes.reserve(2 * objs.size());
+  out.nodes.emplace_back();
+  build(items, 0, items.size(), 0, 0, out, sah, prm);
+  // Leaves whose objects are all plain spheres (no wrapper) get kWorldLeafSpheres: the walk reads
+  // their centre and radius from the compact per-slot records instead of the object records.
+  out.sph.assign(4 * out.objs.size(), 0.0);
+  for (size_t j = 0; j < out.objs.size(); ++j) {
+    const DevObject& o = objs[out.objs[j]];
+    if (o.kind == YART_PRIM_SPHERE && o.n_xf == 0)
+      for (int k = 0; k < 4; ++k) out.sph[4 * j + k] = o.p[k];
+  }
+  for (DevWorldNode& n : out.nodes) {
+    if (n.count == 0) continue;
+    bool all = true;
+    for (uint32_t k = 0; k < n.count; ++k) {
+      const DevObject& o = objs[out.objs[n.first + k]];
+      all = all && o.kind == YART_PRIM_SPHERE && o.n_xf == 0;
+    }
+    n.pad[0] = all ? kWorldLeafSpheres : 0u;
+  }
+  // Each leaf's handle (pad[1]): what the walk needs to take the node without reading its record
+  // (the parent's child-box test reads the handle with the box, and the stack holds handles).
+  for (DevWorldNode& n : out.nodes) {
+    if (n.count > kWorldHandleMaxCount || n.first >= kWorldHandleFirstMask) return false;  // the list walk then
+    n.pad[1] = (n.count << 28) | ((n.pad[0] & kWorldLeafSpheres) ? (1u << 27) : 0u) | n.first;
+  }
+  if (out.nodes[0].count != 0) return false;  // a single leaf: the list walk
+  if (collapse4(out, false) || collapse4(out, true)) return true;
+  if (sah) return build_world_bvh_with(objs, out, false, 2);
+  if (median_leaf < kWorldHandleMaxCount) return build_world_bvh_with(objs, out, false, std::min<size_t>(2 * median_leaf, kWorldHandleMaxCount));
+  return false;
+}
+
+}  // namespace
 
 bool check_world4(const std::vector<DevObject>& objs, const BuiltWorld& w, std::string& err) {
   if (w.nodes4.empty()) { err = "no 4-wide nodes"; return false; }

@@ -12,7 +12,7 @@ from pathlib import Path
 
 import numpy as np
 
-from . import abi
+from . import abi, buildid
 
 PKG_DIR = Path(__file__).resolve().parent.parent
 REPO_DIR = PKG_DIR.parent
@@ -22,6 +22,16 @@ DEFAULT_SEED = 0x59415254  # counter RNG seed for every run
 
 _host = None
 _dev = None
+
+
+class StaleLibraryError(RuntimeError):
+    """libyart.so's yart_build_id() is not the sha256 of this tree's sources (yart/buildid.py)."""
+
+
+def build_id():
+    """(library build id, this tree's source hash)."""
+    L = load_device()
+    return L.yart_build_id().decode(), buildid.build_id()
 
 
 class YartError(RuntimeError):
@@ -70,12 +80,25 @@ def load_device():
     global _dev
     if _dev is not None:
         return _dev
-    path = Path(os.environ.get("YART_DEVICE_LIB", LIB_DIR / "libyart.so"))  # A/B builds (tools/ab.py)
+    variant = os.environ.get("YART_DEVICE_LIB")  # A/B builds (tools/ab.py): a patched tree, its own id
+    path = Path(variant or LIB_DIR / "libyart.so")
     if not path.exists():
         raise FileNotFoundError(f"{path} is not built; the HIP path has no fallback")
     L = C.CDLL(str(path))
     P, U32, U64, D, I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_double, C.c_int
     _sig(L, "yart_version", C.c_char_p)
+    if not variant:
+        # the shipped .so must be the one built from this tree's sources
+        lib_id = "(none: a build without yart_build_id)"
+        if hasattr(L, "yart_build_id"):
+            _sig(L, "yart_build_id", C.c_char_p)
+            lib_id = L.yart_build_id().decode()
+        tree_id = buildid.build_id()
+        if lib_id != tree_id:
+            raise StaleLibraryError(f"{path} was built from other sources (build id {lib_id}) than this tree's "
+                                    f"({tree_id}); run `make`")
+    elif hasattr(L, "yart_build_id"):
+        _sig(L, "yart_build_id", C.c_char_p)
     _sig(L, "yart_last_error", C.c_char_p)
     _sig(L, "yart_device_count", I, C.POINTER(I))
     _sig(L, "yart_scene_create", I, I, C.POINTER(abi.SceneDesc), C.POINTER(P))
@@ -106,6 +129,8 @@ def load_device():
     _sig(L, "yart_multi_frame_timing", I, P, C.POINTER(D), C.POINTER(D), C.POINTER(U32))
     _sig(L, "yart_unpack_shards_async", I, I, P, U32, U64, U32, U32, P, P)
     _sig(L, "yart_multi_last_timing", I, P, C.POINTER(D), C.POINTER(D))
+    if hasattr(L, "yart_multi_device_timing"):  # absent from older A/B builds
+        _sig(L, "yart_multi_device_timing", I, P, I, C.POINTER(D), C.POINTER(D), C.POINTER(U32))
     _sig(L, "yart_multi_destroy", None, P)
     if hasattr(L, "yart_multi_query"):  # diagnostics only (bench.py's watchdog); absent from older A/B builds
         _sig(L, "yart_multi_query", I, P, P, P)
@@ -416,6 +441,14 @@ class MultiScene:
         up = C.c_int32()
         _check_dev(load_device().yart_multi_query(self._m, st, C.byref(up)))
         return list(st), up.value
+
+    def device_timing(self):
+        """yart_multi_device_timing: per device, summed over the frames of the latest frame_timing()
+        read — (render_ms list, own-gather_ms list, frames)."""
+        n = len(self.devices)
+        r, g, f = (C.c_double * n)(), (C.c_double * n)(), C.c_uint32()
+        _check_dev(load_device().yart_multi_device_timing(self._m, n, r, g, C.byref(f)))
+        return list(r), list(g), f.value
 
     def last_timing(self):
         r, g = C.c_double(), C.c_double()

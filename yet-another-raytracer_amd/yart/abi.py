@@ -115,7 +115,7 @@ PROGRESS_FN = C.CFUNCTYPE(None, C.c_uint64, C.c_void_p)
 
 # Every symbol include/yart.h declares (checked by tests/test_abi.py without a GPU).
 DEVICE_SYMBOLS = [
-    "yart_version", "yart_last_error", "yart_device_count", "yart_scene_create", "yart_scene_destroy",
+    "yart_version", "yart_build_id", "yart_multi_device_timing", "yart_last_error", "yart_device_count", "yart_scene_create", "yart_scene_destroy",
     "yart_scene_get_info", "yart_camera_init", "yart_render_async", "yart_frame_timing", "yart_render",
     "yart_render_with_stats",
     "yart_finalize_rgba8_async", "yart_finalize_rgba8", "yart_intersect", "yart_probe_rng", "yart_probe_math",
