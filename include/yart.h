@@ -232,7 +232,10 @@ typedef struct yart_render_stats {
   uint64_t coop_rounds;    /* cooperative QBVH walk: wave rounds (16 quad steps)  */
   uint64_t coop_leaf_rounds; /* ... rounds in which some quad tested a leaf      */
   uint64_t coop_walks;     /* ... wave-level walks started                       */
-  uint64_t reserved[5];
+  uint64_t coop_idle_slots; /* ... quad slots of those rounds holding no ray (the drain) */
+  uint64_t world_iters;    /* world-BVH walk: loop iterations the waves issue (per-lane visits: node_visits, prim_tests) */
+  uint64_t world_leaf_iters; /* ... of them with some lane at a leaf               */
+  uint64_t reserved[2];
 } yart_render_stats;
 
 typedef void (*yart_progress_fn)(uint64_t pixels_done, void* user);

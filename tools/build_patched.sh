@@ -7,7 +7,7 @@ REPO=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; PATCH=$2
 TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
-tar -C "$REPO" -cf - Makefile include yet-another-raytracer_amd/csrc yet-another-raytracer_amd/host tables tools/gen_tables_inc.py | tar -x -C "$TMP"
+tar -C "$REPO" -cf - Makefile include yet-another-raytracer_amd/csrc yet-another-raytracer_amd/host tables tools/gen_tables_inc.py yet-another-raytracer_amd/yart/buildid.py | tar -x -C "$TMP"
 python3 "$PATCH" "$TMP/yet-another-raytracer_amd/csrc/kernels.hip"
 make -C "$TMP" -j8 device > "$TMP/build.log" 2>&1 || { tail -20 "$TMP/build.log"; exit 1; }
 mkdir -p "$REPO/yet-another-raytracer_amd/lib/variants"

@@ -969,8 +969,8 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
   HIP_TRY(hipMemsetAsync(d_out, 0, bytes, stream), "hipMemset");
   if (stats) {
-    HIP_TRY(hipMalloc(&d_stats, 12 * sizeof(unsigned long long)), "hipMalloc stats");
-    HIP_TRY(hipMemsetAsync(d_stats, 0, 12 * sizeof(unsigned long long), stream), "hipMemset");
+    HIP_TRY(hipMalloc(&d_stats, 14 * sizeof(unsigned long long)), "hipMalloc stats");
+    HIP_TRY(hipMemsetAsync(d_stats, 0, 14 * sizeof(unsigned long long), stream), "hipMemset");
   }
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
@@ -989,7 +989,7 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   if (int rc = wait_with_progress({done}, {s->device}, {&pr}, pr.pixels, progress, user)) return rc;
   HIP_TRY(hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, stream), "copy output");
   if (stats) {
-    unsigned long long v[12];
+    unsigned long long v[14];
     HIP_TRY(hipMemcpyAsync(v, d_stats, sizeof v, hipMemcpyDeviceToHost, stream), "copy stats");
     HIP_TRY(hipStreamSynchronize(stream), "copy stats");
     std::memset(stats, 0, sizeof *stats);
@@ -997,6 +997,8 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
     stats->leaf_visits = v[4]; stats->leaf_tris = v[5]; stats->light_tests = v[6];
     stats->mesh_rewalks = v[7];
     stats->coop_rounds = v[8]; stats->coop_leaf_rounds = v[9]; stats->coop_walks = v[10];
+    stats->coop_idle_slots = v[11];
+    stats->world_iters = v[12]; stats->world_leaf_iters = v[13];
   }
   HIP_TRY(hipStreamSynchronize(stream), "copy output");
   return ok();

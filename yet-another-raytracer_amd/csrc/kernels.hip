@@ -685,7 +685,7 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
 }
 
 // --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543)
-constexpr int kNumStats = 12;
+constexpr int kNumStats = 14;
 struct Stats { unsigned long long v[kNumStats]; };
 enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };  // ST_REWALK = 7 below
 
@@ -933,7 +933,8 @@ __device__ __forceinline__ uint32_t quad_rank(float key, uint32_t c) {
 // Test hook (yart_debug_force_rewalk): every ray the post-walk check covers walks again in the
 // reference's order, so the rare path is exercised on whole frames.
 __device__ uint32_t g_force_rewalk;
-enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10 };  // per wave: lane 0 counts
+enum { ST_REWALK = 7, ST_ROUNDS = 8, ST_LEAF_ROUNDS = 9, ST_WALKS = 10, ST_IDLE_SLOTS = 11,  // per wave: lane 0 counts
+       ST_WORLD_ITERS = 12, ST_WORLD_LEAF_ITERS = 13 };  // world-BVH walk: wave-level loop iterations (first active lane)
 #ifdef YART_WALK_CHECK
 // Bounds-checked build of the cooperative walk (tools: make variant DEFS=-DYART_WALK_CHECK): every
 // record / node / stack index is checked before use; a violation sets a bit here (1 leaf record
@@ -1087,11 +1088,13 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
   for (;;) {
     const bool has = ray < n;
     if (__ballot(has) == 0) break;
-    if (STATS) {  // the ballot outside the lane-0 branch: it must see every quad
+    if (STATS) {  // the ballots outside the lane-0 branch: they must see every quad
       const bool any_leaf = __ballot(has && (node >> 31)) != 0;
+      const uint64_t busy = __ballot(has && c == 0u);
       if (lane == 0) {
         st.v[ST_ROUNDS]++;
         st.v[ST_LEAF_ROUNDS] += any_leaf ? 1u : 0u;
+        st.v[ST_IDLE_SLOTS] += 16u - (uint32_t)__popcll(busy);  // the drain: quads without a ray this round
       }
     }
     bool fin = false;
@@ -1532,6 +1535,10 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   int cursor = 0;
   for (;;) {
     const uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
+    if (STATS) {  // SIMT efficiency of the per-lane walk: iterations the wave issues (lane visits: ST_NODES, ST_PRIM)
+      const uint64_t on = __ballot(true), lf = __ballot(count != 0u);
+      if (__lane_id() == (uint32_t)__builtin_ctzll(on)) { st.v[ST_WORLD_ITERS]++; st.v[ST_WORLD_LEAF_ITERS] += lf ? 1u : 0u; }
+    }
     bool pop = true;
     if (count && ((hnd >> 27) & 1u)) {
       // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
@@ -1853,6 +1860,15 @@ __device__ __forceinline__ kcam_ptr kernarg_camera() {
   return (kcam_ptr)(p + kKernargCam);
 }
 __device__ __forceinline__ V3 ld3(const __attribute__((address_space(4))) double* p) { return mk(p[0], p[1], p[2]); }
+// The render arguments the same way (KA_OPAQUE): each use re-reads its field by a scalar load from the
+// kernarg segment, so no field of RenderArgs holds an SGPR across the render loop.
+typedef const __attribute__((address_space(4))) RenderArgs* kargs_ptr;
+__device__ __forceinline__ kargs_ptr kernarg_args() {
+  const __attribute__((address_space(4))) char* p =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (kargs_ptr)(p + (kKernargCam - offsetof(RenderArgs, cam)));
+}
 
 template <class Cam>
 __device__ __forceinline__ Ray camera_ray(const Cam& c, double s, double t, double wl, Rng& g,
@@ -1890,6 +1906,9 @@ __device__ __forceinline__ Ray camera_ray(const Cam& c, double s, double t, doub
 }
 
 __device__ __forceinline__ bool covered(uint32_t x, uint32_t w) {  // main.rs:636-647 crop grid
+  // w opaque: otherwise the 8 crop starts of each axis are hoisted out of the render loop as 16
+  // loop-invariant SGPRs, which the list kernels spill to VGPR lanes for the whole kernel
+  asm volatile("" : "+s"(w));
   const uint32_t cw = w / 8;
 #pragma unroll
   for (uint32_t col = 0; col < 8; ++col) {
@@ -2029,7 +2048,12 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
 // no lane idles while another still has samples of its own pixel left. Safe because each
 // (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
-__global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void k_render(DevScene S, RenderArgs A) {
+__global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void k_render(DevScene S, RenderArgs A_) {
+#if YART_KA_OPAQUE
+#define A (*kernarg_args())
+#else
+#define A A_
+#endif
   __shared__ uint32_t s_stack[HAS_MESH ? 4 * kWaveLdsWords : BVH ? 4 * kStackSlots * 64 : 1];
   // JOBL (the chunked list and world-BVH kernels): a lane's job identity — pixel, sample, block, slot, x, y —
   // lives in LDS ([word][lane] per wave) from its hand-out to its scratch store, read where it is
@@ -2271,6 +2295,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
   }
 }
 
+#undef A
 // ------------------------------------------------------------- wavefront path (mesh scenes)
 // The megakernel's loop split at the world query. k_wf_shade does, for
 // every path of the pool, what k_render does around the query: the record of the hit the last

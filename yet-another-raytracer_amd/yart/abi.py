@@ -90,7 +90,8 @@ class RenderStats(C.Structure):
                 ("node_visits", C.c_uint64), ("leaf_visits", C.c_uint64), ("leaf_tris", C.c_uint64),
                 ("light_tests", C.c_uint64), ("mesh_rewalks", C.c_uint64),
                 ("coop_rounds", C.c_uint64), ("coop_leaf_rounds", C.c_uint64), ("coop_walks", C.c_uint64),
-                ("reserved", C.c_uint64 * 5)]
+                ("coop_idle_slots", C.c_uint64), ("world_iters", C.c_uint64),
+                ("world_leaf_iters", C.c_uint64), ("reserved", C.c_uint64 * 2)]
 
 
 class RenderDefaults(C.Structure):
