@@ -478,6 +478,14 @@ def main():
                     "hbm_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if traffic else None),
                     # the sample scratch k_render writes (24 B of XYZ per sample)
                     "algorithmic_bytes_per_launch": st.samples * 24 if chunked else None,
+                    # SURVEY §8(d)'s record bytes (24 B per rect / box-face / light re-test, 128 B per
+                    # QBVH node, 36 B per leaf triangle): an algorithmic byte RATE served from the
+                    # scalar / L1 caches (the scene is < 4 KB), not HBM traffic — reported beside the
+                    # VALU bound, which is this kernel's roofline
+                    "record_bytes_per_launch": int(24 * (st.prim_tests + st.light_tests) + 128 * st.node_visits +
+                                                   36 * st.leaf_tris),
+                    "record_byte_rate_of_hbm_peak": round((24 * (st.prim_tests + st.light_tests) + 128 * st.node_visits +
+                                                           36 * st.leaf_tris) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "valu_issue_busy": valu_issue(pmc) if world == 1 else None,
                     "fp64_issued": fp64_issue(pmc, kern_ms) if world == 1 else None,
                     # wave-level VALU instructions (SQ_INSTS_VALU of the snapshot) per path segment

@@ -144,6 +144,7 @@ yart_scene::~yart_scene() {
   for (auto& kv : streams) {
     (void)hipFree(kv.second->scratch);
     if (kv.second->wf_mem) (void)hipFree(kv.second->wf_mem);
+    if (kv.second->ovf) (void)hipFree(kv.second->ovf);
     if (kv.second->wf_status_host) (void)hipHostFree(kv.second->wf_status_host);
   }
   for (hipStream_t st : owned_streams) (void)hipStreamDestroy(st);
@@ -296,7 +297,22 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   for (uint32_t m = 0; m < d->n_meshes; ++m) {
     BuiltMesh& b = built[m];
     HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
-    HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
+    if (kDevTriFloats == kTriFloats) {
+      HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
+    } else {  // YART_TRI64: v0, e1, e2 in f64 (device_types.h), then the three words
+      const size_t nr = b.leaves.size() / kTriFloats;
+      std::vector<float> d64(kDevTriFloats * nr, 0.0f);
+      for (size_t r = 0; r < nr; ++r) {
+        const float* f = &b.leaves[kTriFloats * r];
+        const double v0[3] = {(double)f[0], (double)f[1], (double)f[2]};
+        const double vals[9] = {v0[0], v0[1], v0[2], (double)f[3] - v0[0], (double)f[4] - v0[1], (double)f[5] - v0[2],
+                                (double)f[6] - v0[0], (double)f[7] - v0[1], (double)f[8] - v0[2]};
+        float* o = &d64[kDevTriFloats * r];
+        std::memcpy(o, vals, sizeof vals);
+        std::memcpy(o + 18, f + 9, 3 * sizeof(float));
+      }
+      HIP_TRY(upload(s->owned, d64.data(), d64.size(), &dm[m].leaves, bytes), "upload leaves");
+    }
     // Normals from the OBJ's vn lines are f32 values (tobj parses f32): then an f32 table holds them
     // exactly in half the bytes (read once per mesh hit, mesh_rec); computed face normals are f64.
     std::vector<float> n32(b.normals.size());
@@ -352,19 +368,19 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   for (uint32_t i = 0; i < d->n_textures; ++i)
     ds.has_ext |= d->textures[i].kind == YART_TEX_NOISE || d->textures[i].kind == YART_TEX_IMAGE;
 
-  // Mesh scenes: the megakernel by default (A/B r03: the wavefront path is 18 % slower on david and
-  // 47 % on the bunny stand-in); the wavefront path (k_wf_shade / k_wf_trace) for
-  // meshes deeper than depth 10, which need more than the megakernel's 32 stack slots — its trace
-  // kernel walks them with the reference's 64 (qbvh.rs:382-384). YART_OPT_MESH_WAVEFRONT = 1 puts every mesh
-  // scene without EXT features (media, moving spheres, noise / image textures) on the wavefront
-  // path, 0 none (deep meshes are then refused).
+  // Mesh scenes: the megakernel (A/B r03: the wavefront path is 18 % slower on david and 47 % on the
+  // bunny stand-in), meshes deeper than depth 10 included since r05: their walk stacks
+  // keep 32 entries in LDS and overflow into HBM up to the reference's 64 (qbvh.rs:382-384; kernels.hip
+  // OVF). YART_OPT_MESH_WAVEFRONT = 1 puts every mesh scene without EXT features (media, moving spheres,
+  // noise / image textures) on the wavefront path (k_wf_shade / k_wf_trace); -1 (auto) and 0 keep the
+  // megakernel. A deep mesh in an EXT scene is refused (no such megakernel variant).
   {
     const int64_t force = opt(YART_OPT_MESH_WAVEFRONT);
     ds.deep = d->n_meshes && 3 * depth + 1 > (uint32_t)kStackSlots;
-    s->wavefront = ds.has_mesh && !ds.has_ext && (force == 1 || (force != 0 && ds.deep));
-    if (ds.deep && !s->wavefront)
-      return fail(YART_ERR_UNSUPPORTED, "a mesh deeper than depth 10 renders on the wavefront path only (no media, "
-                                        "moving spheres or noise / image textures in its scene, YART_OPT_MESH_WAVEFRONT not 0)");
+    s->wavefront = ds.has_mesh && !ds.has_ext && force == 1;
+    if (ds.deep && ds.has_ext)
+      return fail(YART_ERR_UNSUPPORTED, "a mesh deeper than depth 10 in a scene with media, moving spheres or "
+                                        "noise / image textures");
     const int64_t pool = opt(YART_OPT_WF_POOL);
     if (pool >= 256) s->wf_pool = (uint32_t)(std::min<int64_t>(pool, 1ll << 24) / 256 * 256);
   }
@@ -582,6 +598,21 @@ int stream_scratch(StreamState* st, hipStream_t stream, size_t bytes, double** o
 }
 
 // n timing events for one frame (copied out: the caller owns them until push_frame hands them over).
+// The walk stacks' HBM overflow of a stream (deep meshes), grown on demand like the scratch.
+int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out) {
+  if (st->ovf_bytes < bytes) {
+    if (st->ovf) {
+      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its stack overflow");
+      HIP_TRY(hipFree(st->ovf), "hipFree stack overflow");
+    }
+    st->ovf = nullptr; st->ovf_bytes = 0;
+    HIP_TRY(hipMalloc(&st->ovf, bytes), "hipMalloc stack overflow");
+    st->ovf_bytes = bytes;
+  }
+  *out = st->ovf;
+  return YART_OK;
+}
+
 int take_events(yart_scene* s, size_t n, std::vector<hipEvent_t>& f) {
   f.clear();
   std::lock_guard<std::mutex> lk(s->mu);
@@ -727,8 +758,6 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
   if (prog) { a.progress = prog->device; a.progress_count = prog->counter; }
-  if (stats && s->dev.deep)  // the instrumented megakernel has the 32-slot stack
-    return fail(YART_ERR_UNSUPPORTED, "work counters for a mesh deeper than depth 10");
   if (s->wavefront && !stats) {  // mesh scenes: the wavefront path, pass by pass over the scratch budget
     double* scratch = nullptr;
     const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
@@ -753,6 +782,12 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     if (prog) prog->total_units = 0;
     push_frame(s, stream, std::move(ev));
     return YART_OK;
+  }
+  if (s->dev.deep) {  // the walk stacks' HBM overflow: one region per wave of the largest launch below
+    const uint64_t fused_waves = (uint64_t)a.n_blocks, dyn_waves = (uint64_t)s->cu_count * 16;
+    const uint64_t units = (uint64_t)a.n_blocks * ((pl.pass_spp + pl.chunk - 1) / pl.chunk);
+    const uint64_t waves = (pl.chunk >= a.spp ? fused_waves : std::min(dyn_waves, units)) + 4;
+    if (int rc = stream_ovf(st, stream, waves * kOvfWords * sizeof(uint32_t), &a.stack_ovf)) return rc;
   }
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
     if (prog) prog->total_units = a.n_blocks;

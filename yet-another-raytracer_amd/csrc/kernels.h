@@ -30,7 +30,14 @@ struct RenderArgs {
   uint32_t* progress;         // host-mapped word (null = none): a plain store of base + units claimed
                               // (chunked path) or finished (fused path)
   uint32_t* progress_count;   // fused path with progress: device counter of finished units (zeroed per frame)
+  uint32_t* stack_ovf;        // deep meshes: kOvfWords per wave of the grid (the walk stacks' HBM overflow)
 };
+// Walk-stack overflow of the megakernel for meshes deeper than depth 10 (kernels.hip, qbvh_lane): per
+// wave, the cooperative walk's per-quad stacks past their 32 LDS slots (node ids, then entries) and
+// the reference-order walk's per-lane stacks past theirs, up to the reference's 64 entries.
+constexpr int kOvfQuadWords = (kMaxStackSlots - kStackSlots) * 16;
+constexpr int kOvfLaneWords = (kMaxStackSlots - kStackSlots) * 64;
+constexpr int kOvfWords = 2 * kOvfQuadWords + kOvfLaneWords;
 
 // Shard s of N owns global blocks s, s + N, s + 2N, ... of the ceil(W/8) x ceil(H/8) grid.
 __host__ __device__ inline uint32_t shard_blocks(uint32_t total_blocks, uint32_t shard_index, uint32_t shard_count) {

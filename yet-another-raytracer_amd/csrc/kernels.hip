@@ -722,11 +722,42 @@ __device__ __forceinline__ bool child_hit(float4 lo, float4 hi, const double ro[
 }
 // Möller–Trumbore on one leaf record (hitx4's lane, qbvh.rs:475-540): a hit needs t in
 // [t_min, t_max) — strict at t_max, so an equal t later in the leaf or tree does not replace.
-__device__ __forceinline__ bool leaf_tri_hit(float4 p0, float4 p1, float4 p2, const double ro[3], const double rd[3],
+// A leaf record as the test uses it: v0 and the edges in f64 — formed here from the f32 vertices
+// (kTriFloats layout), or read as the host formed them by the same f64 operations (YART_TRI64).
+struct TriF64 { double v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z; };
+__device__ __forceinline__ double f4d(float a, float b) {
+  return __longlong_as_double((long long)(((uint64_t)__float_as_uint(b) << 32) | __float_as_uint(a)));
+}
+constexpr int kRecF4 = kDevTriFloats / 4;  // float4s per device triangle record
+// Record `i` of a leaf run: its f64 form, and the three words (reference leaf, lane, sorted index).
+__device__ __forceinline__ TriF64 tri_load(gfloat4p R, uint32_t& li, uint32_t& lane, uint32_t& sorted) {
+  TriF64 g;
+  if constexpr (kRecF4 == 3) {
+    float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
+    // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
+    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
+                 "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
+    g.v0x = p0.x; g.v0y = p0.y; g.v0z = p0.z;
+    g.e1x = (double)p0.w - g.v0x; g.e1y = (double)p1.x - g.v0y; g.e1z = (double)p1.y - g.v0z;
+    g.e2x = (double)p1.z - g.v0x; g.e2y = (double)p1.w - g.v0y; g.e2z = (double)p2.x - g.v0z;
+    li = __float_as_uint(p2.y); lane = __float_as_uint(p2.z); sorted = __float_as_uint(p2.w);
+  } else {
+    float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2), p3 = ld4(R, 3), p4 = ld4(R, 4), p5 = ld4(R, 5);
+    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p1.w),
+                 "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z), "+v"(p3.w),
+                 "+v"(p4.x), "+v"(p4.y), "+v"(p4.z), "+v"(p4.w), "+v"(p5.x), "+v"(p5.y), "+v"(p5.z));
+    g.v0x = f4d(p0.x, p0.y); g.v0y = f4d(p0.z, p0.w); g.v0z = f4d(p1.x, p1.y);
+    g.e1x = f4d(p1.z, p1.w); g.e1y = f4d(p2.x, p2.y); g.e1z = f4d(p2.z, p2.w);
+    g.e2x = f4d(p3.x, p3.y); g.e2y = f4d(p3.z, p3.w); g.e2z = f4d(p4.x, p4.y);
+    li = __float_as_uint(p4.z); lane = __float_as_uint(p4.w); sorted = __float_as_uint(p5.x);
+  }
+  return g;
+}
+__device__ __forceinline__ bool leaf_tri_hit(const TriF64& g, const double ro[3], const double rd[3],
                                              double tmin, double tmax, double& t, double& u, double& v) {
-  const double v0x = p0.x, v0y = p0.y, v0z = p0.z;
-  const double e1x = (double)p0.w - v0x, e1y = (double)p1.x - v0y, e1z = (double)p1.y - v0z;
-  const double e2x = (double)p1.z - v0x, e2y = (double)p1.w - v0y, e2z = (double)p2.x - v0z;
+  const double v0x = g.v0x, v0y = g.v0y, v0z = g.v0z;
+  const double e1x = g.e1x, e1y = g.e1y, e1z = g.e1z;
+  const double e2x = g.e2x, e2y = g.e2y, e2z = g.e2z;
   const double hx = rd[1] * e2z - rd[2] * e2y, hy = rd[2] * e2x - rd[0] * e2z, hz = rd[0] * e2y - rd[1] * e2x;
   const double a = e1x * hx + e1y * hy + e1z * hz;
   const double f = 1.0 / a;
@@ -746,10 +777,16 @@ __device__ __forceinline__ bool leaf_tri_hit(float4 p0, float4 p1, float4 p2, co
 // through references, the caller's Ray and hit variables became stack objects, written to scratch
 // at every mesh walk of the world pass whether or not the re-walk ran.
 struct LaneHit { double t, u, v; uint32_t tri, found; };
-template <bool STATS>
+// Deep meshes in the megakernel (OVF): the traversal stacks keep their first kStackSlots entries in
+// LDS and the rest — up to the reference's 64 (qbvh.rs:382-384) — in a per-wave HBM region
+// (RenderArgs::stack_ovf, kOvfWords per resident wave): the per-quad stacks of the cooperative walk
+// ([slot - 32][quad] node ids, then their 16-bit entries) and the per-lane stacks of the reference-
+// order walk ([slot - 32][lane]). Entries past slot 32 are pushed only by walks deeper than depth 10,
+// so the LDS budget — and with it 4 waves per SIMD — is that of every other mesh (kOvf*: kernels.h).
+template <bool STATS, bool OVF = false>
 __device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double ox, double oy, double oz, double dx,
                                           double dy, double dz, double tmin, double tmax, uint32_t* __restrict__ stk,
-                                          unsigned long long* __restrict__ stv) {
+                                          unsigned long long* __restrict__ stv, uint32_t* __restrict__ ovf = nullptr) {
   const DevMesh& M = *Mp;
   const double ro[3] = {ox, oy, oz}, rd[3] = {dx, dy, dz};
   const double inv[3] = {1.0 / rd[0], 1.0 / rd[1], 1.0 / rd[2]};
@@ -760,15 +797,18 @@ __device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double
   int cursor = 0;
   stk[0] = M.root;
   for (;;) {
-    const uint32_t id = stk[cursor * 64];
+    uint32_t id;
+    if (!OVF || cursor < kStackSlots) id = stk[cursor * 64];
+    else id = ovf[(cursor - kStackSlots) * 64];  // OVF: ovf is this lane's column of the wave's lane stacks
     if (id >> 31) {
       const uint32_t count = (id >> 27) & 0xFu, first = id & ((1u << 27) - 1u);
-      const gfloat4p L = leaves + 3 * (size_t)first;
+      const gfloat4p L = leaves + kRecF4 * (size_t)first;
       if (STATS) { stv[ST_LEAVES]++; stv[ST_LEAF_TRIS] += count; }
       for (uint32_t i = 0; i < count; ++i) {  // the running t_max: the first of equal hits stays
         double t, u, v;
-        const float4 p2 = ld4(L, 3 * i + 2);
-        if (leaf_tri_hit(ld4(L, 3 * i), ld4(L, 3 * i + 1), p2, ro, rd, tmin, tmax, t, u, v)) {
+        uint32_t li, ln, so;
+        const TriF64 g = tri_load(L + kRecF4 * i, li, ln, so);
+        if (leaf_tri_hit(g, ro, rd, tmin, tmax, t, u, v)) {
           tmax = t;
           hit.t = t; hit.u = u; hit.v = v;
           hit.tri = first + i;
@@ -789,8 +829,13 @@ __device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double
         ordered |= (hk[k] ? 1u : 0u) << rank[k];
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)  // pushed in rank order: slot = hit children of lower rank
-        if (hk[k]) stk[(cursor + (int)__popc(ordered & ((1u << rank[k]) - 1u))) * 64] = chs[k];
+      for (int k = 0; k < 4; ++k) {  // pushed in rank order: slot = hit children of lower rank
+        const int slot = cursor + (int)__popc(ordered & ((1u << rank[k]) - 1u));
+        if (hk[k]) {
+          if (!OVF || slot < kStackSlots) stk[slot * 64] = chs[k];
+          else ovf[(slot - kStackSlots) * 64] = chs[k];
+        }
+      }
       cursor += (int)__popc(ordered);
     }
     if (cursor == 0) break;
@@ -799,10 +844,13 @@ __device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double
   hit.found = found ? 1u : 0u;
   return hit;
 }
-template <bool STATS>
+template <bool STATS, bool OVF = false>
 __device__ __forceinline__ bool qbvh_t(const DevMesh& M, const Ray& r, double tmin, double tmax, double& t_hit,
-                                       uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st) {
-  const LaneHit h = qbvh_lane<STATS>(&M, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, tmin, tmax, stk, STATS ? st.v : nullptr);
+                                       uint32_t& tri, double& u_hit, double& v_hit, uint32_t* __restrict__ stk, Stats& st,
+                                       uint32_t* __restrict__ ovf = nullptr) {
+  // ovf: the wave's overflow region; this lane's column of its lane stacks
+  const LaneHit h = qbvh_lane<STATS, OVF>(&M, r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, tmin, tmax, stk, STATS ? st.v : nullptr,
+                                          OVF ? ovf + 2 * kOvfQuadWords + __lane_id() : nullptr);
   if (h.found) { t_hit = h.t; u_hit = h.u; v_hit = h.v; tri = h.tri; }
   return h.found != 0u;
 }
@@ -1017,10 +1065,10 @@ __device__ __forceinline__ bool coop_check(const __attribute__((address_space(1)
   return h > l && t >= l;
 }
 // Inlined: +4 % david, +11 % bunny over a call (the call site spills the caller's state).
-template <bool STATS, int SLOTS = kCoopSlots>
+template <bool STATS, int SLOTS = kCoopSlots, bool OVF = false>
 __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
-                                       uint8_t* __restrict__ lds, Stats& st) {
+                                       uint8_t* __restrict__ lds, Stats& st, uint32_t* __restrict__ ovf = nullptr) {
   found = false;
   if (__ballot(want) == 0) return;
   const uint32_t lane = __lane_id();
@@ -1115,12 +1163,9 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
         uint32_t kk, id, li = 0u;  // li is read across the quad (ds_bpermute): defined in every lane
         bool cand = false;
         if (c < count) {
-          const gfloat4p R = leaves + 3 * (size_t)(first + c);
-          float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
-          // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
-          asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
-                       "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
-          li = __float_as_uint(p2.y);  // the record's reference leaf
+          const gfloat4p R = leaves + kRecF4 * (size_t)(first + c);
+          uint32_t ln, so;
+          const TriF64 g = tri_load(R, li, ln, so);  // li: the record's reference leaf
 #ifdef YART_WALK_CHECK
           if (li >= M.n_leaves) { walk_fault(2u); li = 0u; }
 #endif
@@ -1128,10 +1173,10 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
           // back: the tie goes to the reference's visiting order)
           const CoopRay& s = rays[ray];
           const double ro[3] = {s.o[0], s.o[1], s.o[2]}, rd[3] = {s.d[0], s.d[1], s.d[2]};
-          if (leaf_tri_hit(p0, p1, p2, ro, rd, tmin, s.tmax, tt, u, v) && (tt < tb || (f2b && tt == tb))) {
+          if (leaf_tri_hit(g, ro, rd, tmin, s.tmax, tt, u, v) && (tt < tb || (f2b && tt == tb))) {
             cand = true;
-            id = __float_as_uint(p2.w);  // sorted index: the normal table's row
-            kk = f2b ? (aux[li].rank[pos] << 4) | (__float_as_uint(p2.z) << 2) | c : c;
+            id = so;  // sorted index: the normal table's row
+            kk = f2b ? (aux[li].rank[pos] << 4) | (ln << 2) | c : c;
           }
         }
         double t = cand ? tt : INFINITY;
@@ -1198,22 +1243,26 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
           nx |= quad_perm<0xB1>(nx);
           nx |= quad_perm<0x4E>(nx);
           if (hk && rk != last) {
-            const int slot = (cursor + (int)__popc(ordered & ((1u << rk) - 1u))) * 16 + (int)q;
+            const int depth_slot = cursor + (int)__popc(ordered & ((1u << rk) - 1u));
+            const int slot = depth_slot * 16 + (int)q;
+            // rounded down: a dropped entry's true entry is beyond the bound too
+            const uint32_t eb = __float_as_uint(ent);
+            const uint32_t e16 = (eb >> 16) + ((eb >> 31) & ((eb & 0xFFFFu) != 0u));
 #ifdef YART_WALK_CHECK
-            if (slot >= SLOTS * 16) walk_fault(8u);
+            if (depth_slot >= (OVF ? kMaxStackSlots : SLOTS)) walk_fault(8u);
             else
 #endif
-            {
+            if (!OVF || depth_slot < SLOTS) {
               qstk[slot] = child;
-              {  // rounded down: a dropped entry's true entry is beyond the bound too
-                const uint32_t eb = __float_as_uint(ent);
-                qent[slot] = (CoopEnt)((eb >> 16) + ((eb >> 31) & ((eb & 0xFFFFu) != 0u)));
-              }
+              qent[slot] = (CoopEnt)e16;
+            } else {  // deep meshes: entries past the LDS slots in the wave's HBM region
+              ovf[slot - SLOTS * 16] = child;
+              ovf[kOvfQuadWords + slot - SLOTS * 16] = e16;
             }
           }
           cursor += (int)__popc(ordered) - 1;
 #ifdef YART_WALK_CHECK
-          if (cursor >= SLOTS) cursor = SLOTS - 1;
+          if (cursor >= (OVF ? kMaxStackSlots : SLOTS)) cursor = (OVF ? kMaxStackSlots : SLOTS) - 1;
 #endif
           node = nx;
           popped = true;
@@ -1223,8 +1272,15 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
         for (;;) {  // front to back: entries whose box begins beyond the bound are dropped
           if (cursor == 0) { fin = true; break; }
           cursor -= 1;
-          node = qstk[cursor * 16 + (int)q];
-          if (!f2b || !(__uint_as_float((uint32_t)qent[cursor * 16 + (int)q] << 16) > bound)) break;
+          uint32_t e16;
+          if (!OVF || cursor < SLOTS) {
+            node = qstk[cursor * 16 + (int)q];
+            e16 = qent[cursor * 16 + (int)q];
+          } else {
+            node = ovf[(cursor - SLOTS) * 16 + (int)q];
+            e16 = ovf[kOvfQuadWords + (cursor - SLOTS) * 16 + (int)q];
+          }
+          if (!f2b || !(__uint_as_float(e16 << 16) > bound)) break;
         }
       }
       if (kPostCheck && fin && c == 0)  // the ray's own lane checks W after the walk (below)
@@ -1283,7 +1339,7 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (redo) {
       if (STATS) st.v[ST_REWALK]++;
-      found = qbvh_t<STATS>(M, wr, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st);
+      found = qbvh_t<STATS, OVF>(M, wr, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st, ovf);
     }
   }
 }
@@ -1321,10 +1377,10 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 // u, v; the mesh kernels carry u, v and the triangle (a mesh hit's walk result) through the pass.
 struct HitId { double t, u, v; uint32_t obj, sub; };
 
-template <bool HAS_MESH, bool STATS>
+template <bool HAS_MESH, bool STATS, bool OVF = false>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
                                        double tmin, double tmax, double& t, uint32_t& sub, double& u, double& v,
-                                       uint32_t* stk, Stats& st) {
+                                       uint32_t* stk, Stats& st, uint32_t* ovf = nullptr) {
   switch (kind) {
     case YART_PRIM_SPHERE: if (STATS) st.v[ST_PRIM]++; return sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1>(o.p, r, tmin, tmax, t);
@@ -1334,7 +1390,7 @@ __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, ui
     case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
     case YART_PRIM_MOVING_SPHERE: if (STATS) st.v[ST_PRIM]++; return moving_sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_MESH:
-      if constexpr (HAS_MESH) return qbvh_t<STATS>(S.meshes[o.mesh], r, tmin, tmax, t, sub, u, v, stk, st);
+      if constexpr (HAS_MESH) return qbvh_t<STATS, OVF>(S.meshes[o.mesh], r, tmin, tmax, t, sub, u, v, stk, st, ovf);
       return false;
   }
   return false;
@@ -1367,14 +1423,14 @@ __device__ __forceinline__ Ray to_local(const DevObject& o, uint32_t nxf, const 
 // ConstantMedium::hit (hittable.rs:277-318): the boundary (the wrapper chain below the medium
 // and the primitive) hit twice, the entry/exit clamped to [t_min, t_max] and 0, and a free path
 // -1/density · ln(ξ) against the distance inside. xf[0][0] holds -1/density.
-template <bool HAS_MESH, bool STATS>
+template <bool HAS_MESH, bool STATS, bool OVF = false>
 __device__ __forceinline__ bool medium_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& lr, const Ray& r,
                                          double tmin, double tmax, double& t, uint32_t* stk, Stats& st,
-                                         const QueryCtx& q, uint32_t obj) {
+                                         const QueryCtx& q, uint32_t obj, uint32_t* ovf = nullptr) {
   double t1, t2, u, v;
   uint32_t sub;
-  if (!prim_t<HAS_MESH, STATS>(S, o, kind, lr, -INFINITY, INFINITY, t1, sub, u, v, stk, st)) return false;
-  if (!prim_t<HAS_MESH, STATS>(S, o, kind, lr, t1 + 0.0001, INFINITY, t2, sub, u, v, stk, st)) return false;
+  if (!prim_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, -INFINITY, INFINITY, t1, sub, u, v, stk, st, ovf)) return false;
+  if (!prim_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, t1 + 0.0001, INFINITY, t2, sub, u, v, stk, st, ovf)) return false;
   if (t1 < tmin) t1 = tmin;
   if (t2 > tmax) t2 = tmax;
   if (!(t1 < t2)) return false;
@@ -1403,9 +1459,10 @@ __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
   return *(const T*)((cptr)base + __builtin_amdgcn_readfirstlane(i));
 }
 
-template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots>
+template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
-                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
+                                              uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
+                                              uint32_t* ovf = nullptr) {
   bool found = false;
   double closest = tmax;
   uint32_t who = 0;  // obj << 3 | sub (the kernels without meshes)
@@ -1419,7 +1476,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-      qbvh_coop<STATS, SLOTS>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st);
+      qbvh_coop<STATS, SLOTS, OVF>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st, ovf);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1429,8 +1486,8 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       const Ray lr = to_local(o, nxf, r);
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
-      const bool hit = medium ? medium_t<HAS_MESH, STATS>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i)
-                              : prim_t<HAS_MESH, STATS>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st);
+      const bool hit = medium ? medium_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i, ovf)
+                              : prim_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, ovf);
       if (hit) {
         closest = t;
         if (HAS_MESH) { id.obj = i; id.sub = sub; id.u = u; id.v = v; }
@@ -1578,25 +1635,32 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       const float4 mg = ld4(N, 6), hd = ld4(N, 7);
       const float mk[4] = {mg.x, mg.y, mg.z, mg.w};
       const uint32_t ch[4] = {__float_as_uint(hd.x), __float_as_uint(hd.y), __float_as_uint(hd.z), __float_as_uint(hd.w)};
-      // per child: the binary tree's test of that node (the same expression on the same box)
+      // per child: the binary tree's test of that node (the same expression on the same box),
+      // two children at a time in packed f32 (v_pk_add_f32 / v_pk_mul_f32: children 0-1 and 2-3
+      // of one axis are adjacent in DevWorldNode4); only the min / max stay per child
       float key[4];  // entry of a hit child, +inf for a miss
       uint32_t hc[4];
+      const vfloat2 m01 = (vfloat2{mk[0], mk[1]} + (vfloat2)(O)) * (vfloat2)(0x1p-12f);
+      const vfloat2 m23 = (vfloat2{mk[2], mk[3]} + (vfloat2)(O)) * (vfloat2)(0x1p-12f);
+      float lo[4] = {tlo, tlo, tlo, tlo}, hi[4] = {thi, thi, thi, thi};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float m = (mk[k] + O) * 0x1p-12f;
-        float lo = tlo, hi = thi;
+      for (int j = 0; j < 3; ++j) {
+        if (use[j]) {
+          const vfloat2 oj = (vfloat2)(o[j]), ij = (vfloat2)(inv[j]);
+          const vfloat2 a0 = (vfloat2{bmn[j].x, bmn[j].y} - m01 - oj) * ij, a1 = (vfloat2{bmx[j].x, bmx[j].y} + m01 - oj) * ij;
+          const vfloat2 b0 = (vfloat2{bmn[j].z, bmn[j].w} - m23 - oj) * ij, b1 = (vfloat2{bmx[j].z, bmx[j].w} + m23 - oj) * ij;
+          const float t0[4] = {a0.x, a0.y, b0.x, b0.y}, t1[4] = {a1.x, a1.y, b1.x, b1.y};
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (use[j]) {
-            const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
-            const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
-            const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
-            lo = fmaxf(lo, fminf(t0, t1));
-            hi = fminf(hi, fmaxf(t0, t1));
+          for (int k = 0; k < 4; ++k) {
+            lo[k] = fmaxf(lo[k], fminf(t0[k], t1[k]));
+            hi[k] = fminf(hi[k], fmaxf(t0[k], t1[k]));
           }
         }
-        const bool hit = lo <= hi && ch[k] != kWorld4Empty;
-        key[k] = hit ? fminf(lo, 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool hit = lo[k] <= hi[k] && ch[k] != kWorld4Empty;
+        key[k] = hit ? fminf(lo[k], 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
         hc[k] = ch[k];
       }
       if (STATS) st.v[ST_NODES]++;
@@ -1629,14 +1693,15 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, int SLOTS = kCoopSlots>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
-                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q) {
+                                          int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
+                                          uint32_t* ovf = nullptr) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, SLOTS>(S, want, r, tmin, tmax, id, stk, coop, st, q) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, SLOTS, OVF>(S, want, r, tmin, tmax, id, stk, coop, st, q, ovf) || !want) return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -1860,8 +1925,11 @@ __device__ __forceinline__ kcam_ptr kernarg_camera() {
   return (kcam_ptr)(p + kKernargCam);
 }
 __device__ __forceinline__ V3 ld3(const __attribute__((address_space(4))) double* p) { return mk(p[0], p[1], p[2]); }
-// The render arguments the same way (KA_OPAQUE): each use re-reads its field by a scalar load from the
-// kernarg segment, so no field of RenderArgs holds an SGPR across the render loop.
+// The render arguments the same way (YART_KA_OPAQUE, default on): each use re-reads its field by a
+// scalar load from the kernarg segment, so no field of RenderArgs holds an SGPR across the render loop.
+#ifndef YART_KA_OPAQUE
+#define YART_KA_OPAQUE 1
+#endif
 typedef const __attribute__((address_space(4))) RenderArgs* kargs_ptr;
 __device__ __forceinline__ kargs_ptr kernarg_args() {
   const __attribute__((address_space(4))) char* p =
@@ -2047,8 +2115,13 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
 // wave assigning consecutive job ids to the lanes that asked with one ballot + mbcnt prefix — so
 // no lane idles while another still has samples of its own pixel left. Safe because each
 // (pixel, sample) owns its RNG stream and its scratch slot; k_accumulate restores sample order.
-template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT>
+// DEEP: a mesh deeper than depth 10 (DevScene::deep) — the walk stacks overflow into HBM (OVF above).
+template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT, bool DEEP = false>
 __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void k_render(DevScene S, RenderArgs A_) {
+  // The render arguments are read where used, through the opaque kernarg pointer (kernarg_args):
+  // SGPR spills of the chunked list kernel 45 -> 26, world BVH 71 -> 56, mesh 80 -> 60; cornell
+  // 800x800x256 29.16 -> 28.84 ms, the mesh kernels +0.2-0.4 %, random-scene -1 % (noise level;
+  // profiles/r05_ab_covered_ka.log, r05_ab_ka256.log). YART_KA_OPAQUE=0 builds the plain form.
 #if YART_KA_OPAQUE
 #define A (*kernarg_args())
 #else
@@ -2084,6 +2157,8 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
   constexpr bool JL = JOBL || JOBL3;
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
+  // DEEP: this wave's HBM stack region (one per resident wave: the grid's waves, capi.cpp launch_frame)
+  uint32_t* const ovf = DEEP ? A.stack_ovf + (size_t)(blockIdx.x * 4u + wave) * kOvfWords : nullptr;
   Stats st;
   if (STATS) for (int i = 0; i < kNumStats; ++i) st.v[i] = 0;
 
@@ -2220,7 +2295,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
       bool scat = false;
       const QueryCtx q{g.k0, g.k1, JL ? jl[64] : smp, JL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT, kCoopSlots, DEEP>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q, ovf);
       } else if (want) {
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       }
@@ -2690,7 +2765,12 @@ hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hip
     else if (dyn) hipLaunchKernelGGL((k_render<MESH, BVH, false, true, EXT>), dim3(grid), dim3(256), 0, stream, s, a); \
     else hipLaunchKernelGGL((k_render<MESH, BVH, false, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);        \
   } while (0)
-  if (s.has_mesh) {
+  if (s.has_mesh && s.deep && !s.has_ext) {  // deep meshes: stacks overflow into a.stack_ovf (capi.cpp)
+    if (!a.stack_ovf) return hipErrorInvalidValue;
+    if (stats) hipLaunchKernelGGL((k_render<true, false, true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (dyn) hipLaunchKernelGGL((k_render<true, false, false, true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else hipLaunchKernelGGL((k_render<true, false, false, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+  } else if (s.has_mesh) {
     if (s.has_ext) YART_LAUNCH(true, false, true); else YART_LAUNCH(true, false, false);
   } else if (s.world_nodes) {
     if (s.has_ext) YART_LAUNCH(false, true, true); else YART_LAUNCH(false, true, false);  // noise textures only

@@ -47,6 +47,9 @@ struct StreamState {
   uint32_t* wf_status_host = nullptr;
   uint32_t* wf_status_dev = nullptr;
   uint64_t wf_iter = 0;  // wavefront iterations launched on this stream so far (status-ring slot numbering)
+  // deep meshes on the megakernel: the walk stacks' HBM overflow, kOvfWords per wave of a launch
+  uint32_t* ovf = nullptr;
+  size_t ovf_bytes = 0;
 };
 
 // Progress of one frame (yart_render's callback): the kernels store `base + units handed out` to
