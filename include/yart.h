@@ -263,7 +263,7 @@ int yart_camera_init(yart_camera* cam, const double lookfrom[3], const double lo
  * d_xyz_sum: width*height*3 doubles on the scene's device, per-pixel sums of the sanitised
  * sample XYZ (main.rs:690-708). Only this shard's blocks are written; the caller zeroes the
  * buffer if it wants the rest to read 0. Asynchronous: returns after the launch — except on the
- * wavefront path (meshes deeper than depth 10, or YART_OPT_MESH_WAVEFRONT = 1), whose number of
+ * wavefront path (YART_OPT_MESH_WAVEFRONT = 1), whose number of
  * iterations is data-dependent: there the calling thread stays in the launch loop until the frame's
  * last iteration is queued (the device may still be finishing it on return), and progress words
  * move only at the end of the frame. The same holds for yart_render_packed_async and
@@ -455,8 +455,9 @@ enum {
   YART_OPT_WALK_TREE = 2,      /* 1 | 0: build the SAH walk tree / walk the reference tree front to back */
   YART_OPT_MESH_WALK_REF = 3,  /* 0 | 1: every mesh ray walks in the reference's order (qbvh.rs:381-543) */
   YART_OPT_WORLD_BVH = 4,      /* -1 auto (>= 16 objects, no mesh) | 0 never | 1 whenever every object has a box */
-  YART_OPT_MESH_WAVEFRONT = 5, /* -1 auto (meshes deeper than depth 10) | 0 never (those are refused) |
-                                  1 every mesh scene without media / moving spheres / noise or image textures */
+  YART_OPT_MESH_WAVEFRONT = 5, /* -1 / 0: the megakernel for every mesh scene (deep meshes included, their walk
+                                  stacks overflowing into HBM) | 1: the wavefront path for every mesh scene
+                                  without media / moving spheres / noise or image textures */
   YART_OPT_WF_POOL = 6,        /* wavefront path slots, >= 256 (rounded down to a multiple of 256), default 2^20 */
   YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass in bytes, default 4 GiB        */
   YART_OPT_COUNT = 8

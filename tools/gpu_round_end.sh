@@ -10,12 +10,13 @@
 #   prof_cornell_more  stall / memory-instruction passes over bench.py (not in the default steps)
 #   prof_c4 / prof_c5  trace + FETCH / WRITE passes over the C4 / C5 frames tools/bench_configs.py
 #            times at --spp-scale 0.0625 (bunny 800x800x32, david 1920x1080x64)
+#   rehearse bench.py's per-rank N = 2 path on one GPU (both ranks on device 0, gloo gather)
 #   configs  tools/bench_configs.py over every BASELINE config; with PMC summaries of the C4 / C5
 #            frames present in profiles/ (tools/summarize_profiles.py), the counter HBM bytes too
 # Raw outputs under gpurun_out/; tools/summarize_profiles.py turns them into profiles/ files.
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$REPO/gpurun_out; mkdir -p "$OUT"; cd "$REPO"
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 run() {
   local name=$1 limit=$2; shift 2
   timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
@@ -35,6 +36,8 @@ for s in $STEPS; do
     prof_david) PFX=david_ PROG="tools/render_once.py david 960 540 16 2" PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
     prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
     prof_c5) PFX=c5_ PROG="tools/render_once.py david 1920 1080 64 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;
+    rehearse) run ${TAG}_rehearse_n2 300 env YART_BENCH_SAME_DEVICE=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --cpu-spp 0 ;;
     configs)
       PM=""
       [ -f profiles/${TAG}_c4_pmc.json ] && PM="$PM --pmc C4=profiles/${TAG}_c4_pmc.json"

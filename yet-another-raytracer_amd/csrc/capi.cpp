@@ -297,22 +297,7 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   for (uint32_t m = 0; m < d->n_meshes; ++m) {
     BuiltMesh& b = built[m];
     HIP_TRY(upload(s->owned, b.nodes.data(), b.nodes.size(), &dm[m].nodes, bytes), "upload nodes");
-    if (kDevTriFloats == kTriFloats) {
-      HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
-    } else {  // YART_TRI64: v0, e1, e2 in f64 (device_types.h), then the three words
-      const size_t nr = b.leaves.size() / kTriFloats;
-      std::vector<float> d64(kDevTriFloats * nr, 0.0f);
-      for (size_t r = 0; r < nr; ++r) {
-        const float* f = &b.leaves[kTriFloats * r];
-        const double v0[3] = {(double)f[0], (double)f[1], (double)f[2]};
-        const double vals[9] = {v0[0], v0[1], v0[2], (double)f[3] - v0[0], (double)f[4] - v0[1], (double)f[5] - v0[2],
-                                (double)f[6] - v0[0], (double)f[7] - v0[1], (double)f[8] - v0[2]};
-        float* o = &d64[kDevTriFloats * r];
-        std::memcpy(o, vals, sizeof vals);
-        std::memcpy(o + 18, f + 9, 3 * sizeof(float));
-      }
-      HIP_TRY(upload(s->owned, d64.data(), d64.size(), &dm[m].leaves, bytes), "upload leaves");
-    }
+    HIP_TRY(upload(s->owned, b.leaves.data(), b.leaves.size(), &dm[m].leaves, bytes), "upload leaves");
     // Normals from the OBJ's vn lines are f32 values (tobj parses f32): then an f32 table holds them
     // exactly in half the bytes (read once per mesh hit, mesh_rec); computed face normals are f64.
     std::vector<float> n32(b.normals.size());

@@ -67,13 +67,7 @@ static_assert(sizeof(DevNode) == 128, "DevNode must be 128 B");
 // (walk_tree.cpp). A leaf is the run [first, first + count) its node id names
 // (1<<31 | count<<27 | first); lane k of a quad reads record first + k.
 constexpr int kTriFloats = 12;
-// The device's copy of those records (YART_TRI64, an A/B option): the f64 values the leaf test forms
-// from them — v0 and the edges e1 = v1 - v0, e2 = v2 - v0 as f64 subtractions of the f32 inputs, the
-// same operations the kernel would do, so the same bits — then the three words; 96 B, 6 float4s.
-#ifndef YART_TRI64
-#define YART_TRI64 0
-#endif
-constexpr int kDevTriFloats = YART_TRI64 ? 24 : kTriFloats;
+
 
 // Per-leaf side record for the front-to-back walk (qbvh_coop): the leaf's box exactly as its
 // parent stores it, and the leaf's position in the reference's traversal order for each of the

@@ -722,35 +722,22 @@ __device__ __forceinline__ bool child_hit(float4 lo, float4 hi, const double ro[
 }
 // Möller–Trumbore on one leaf record (hitx4's lane, qbvh.rs:475-540): a hit needs t in
 // [t_min, t_max) — strict at t_max, so an equal t later in the leaf or tree does not replace.
-// A leaf record as the test uses it: v0 and the edges in f64 — formed here from the f32 vertices
-// (kTriFloats layout), or read as the host formed them by the same f64 operations (YART_TRI64).
+// A leaf record as the test uses it: v0 and the edges in f64, formed from the f32 vertices. (Records
+// holding these f64 values, formed on the host by the same operations — 96 B instead of 48 —
+// lost 2-3 % on david in r05: the BLAS no longer fits the L2; profiles/r05_ab_tri64.log.)
 struct TriF64 { double v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z; };
-__device__ __forceinline__ double f4d(float a, float b) {
-  return __longlong_as_double((long long)(((uint64_t)__float_as_uint(b) << 32) | __float_as_uint(a)));
-}
-constexpr int kRecF4 = kDevTriFloats / 4;  // float4s per device triangle record
+constexpr int kRecF4 = kTriFloats / 4;  // float4s per triangle record
 // Record `i` of a leaf run: its f64 form, and the three words (reference leaf, lane, sorted index).
 __device__ __forceinline__ TriF64 tri_load(gfloat4p R, uint32_t& li, uint32_t& lane, uint32_t& sorted) {
   TriF64 g;
-  if constexpr (kRecF4 == 3) {
-    float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
-    // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
-    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
-                 "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
-    g.v0x = p0.x; g.v0y = p0.y; g.v0z = p0.z;
-    g.e1x = (double)p0.w - g.v0x; g.e1y = (double)p1.x - g.v0y; g.e1z = (double)p1.y - g.v0z;
-    g.e2x = (double)p1.z - g.v0x; g.e2y = (double)p1.w - g.v0y; g.e2z = (double)p2.x - g.v0z;
-    li = __float_as_uint(p2.y); lane = __float_as_uint(p2.z); sorted = __float_as_uint(p2.w);
-  } else {
-    float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2), p3 = ld4(R, 3), p4 = ld4(R, 4), p5 = ld4(R, 5);
-    asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p1.w),
-                 "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z), "+v"(p3.w),
-                 "+v"(p4.x), "+v"(p4.y), "+v"(p4.z), "+v"(p4.w), "+v"(p5.x), "+v"(p5.y), "+v"(p5.z));
-    g.v0x = f4d(p0.x, p0.y); g.v0y = f4d(p0.z, p0.w); g.v0z = f4d(p1.x, p1.y);
-    g.e1x = f4d(p1.z, p1.w); g.e1y = f4d(p2.x, p2.y); g.e1z = f4d(p2.z, p2.w);
-    g.e2x = f4d(p3.x, p3.y); g.e2y = f4d(p3.z, p3.w); g.e2z = f4d(p4.x, p4.y);
-    li = __float_as_uint(p4.z); lane = __float_as_uint(p4.w); sorted = __float_as_uint(p5.x);
-  }
+  float4 p0 = ld4(R, 0), p1 = ld4(R, 1), p2 = ld4(R, 2);
+  // one wait for the whole record (left alone, the compiler splits it into dependent rounds)
+  asm volatile("" : "+v"(p0.x), "+v"(p0.y), "+v"(p0.z), "+v"(p0.w), "+v"(p1.x), "+v"(p1.y),
+               "+v"(p1.z), "+v"(p1.w), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p2.w));
+  g.v0x = p0.x; g.v0y = p0.y; g.v0z = p0.z;
+  g.e1x = (double)p0.w - g.v0x; g.e1y = (double)p1.x - g.v0y; g.e1z = (double)p1.y - g.v0z;
+  g.e2x = (double)p1.z - g.v0x; g.e2y = (double)p1.w - g.v0y; g.e2z = (double)p2.x - g.v0z;
+  li = __float_as_uint(p2.y); lane = __float_as_uint(p2.z); sorted = __float_as_uint(p2.w);
   return g;
 }
 __device__ __forceinline__ bool leaf_tri_hit(const TriF64& g, const double ro[3], const double rd[3],
@@ -1635,32 +1622,27 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       const float4 mg = ld4(N, 6), hd = ld4(N, 7);
       const float mk[4] = {mg.x, mg.y, mg.z, mg.w};
       const uint32_t ch[4] = {__float_as_uint(hd.x), __float_as_uint(hd.y), __float_as_uint(hd.z), __float_as_uint(hd.w)};
-      // per child: the binary tree's test of that node (the same expression on the same box),
-      // two children at a time in packed f32 (v_pk_add_f32 / v_pk_mul_f32: children 0-1 and 2-3
-      // of one axis are adjacent in DevWorldNode4); only the min / max stay per child
+      // per child: the binary tree's test of that node (the same expression on the same box). (A
+      // packed-f32 form, two children per v_pk_add_f32 / v_pk_mul_f32, lost 3 % on the random scene
+      // in r05: profiles/r05_ab_world_packed.log.)
       float key[4];  // entry of a hit child, +inf for a miss
       uint32_t hc[4];
-      const vfloat2 m01 = (vfloat2{mk[0], mk[1]} + (vfloat2)(O)) * (vfloat2)(0x1p-12f);
-      const vfloat2 m23 = (vfloat2{mk[2], mk[3]} + (vfloat2)(O)) * (vfloat2)(0x1p-12f);
-      float lo[4] = {tlo, tlo, tlo, tlo}, hi[4] = {thi, thi, thi, thi};
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (use[j]) {
-          const vfloat2 oj = (vfloat2)(o[j]), ij = (vfloat2)(inv[j]);
-          const vfloat2 a0 = (vfloat2{bmn[j].x, bmn[j].y} - m01 - oj) * ij, a1 = (vfloat2{bmx[j].x, bmx[j].y} + m01 - oj) * ij;
-          const vfloat2 b0 = (vfloat2{bmn[j].z, bmn[j].w} - m23 - oj) * ij, b1 = (vfloat2{bmx[j].z, bmx[j].w} + m23 - oj) * ij;
-          const float t0[4] = {a0.x, a0.y, b0.x, b0.y}, t1[4] = {a1.x, a1.y, b1.x, b1.y};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            lo[k] = fmaxf(lo[k], fminf(t0[k], t1[k]));
-            hi[k] = fminf(hi[k], fmaxf(t0[k], t1[k]));
-          }
-        }
-      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const bool hit = lo[k] <= hi[k] && ch[k] != kWorld4Empty;
-        key[k] = hit ? fminf(lo[k], 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
+        const float m = (mk[k] + O) * 0x1p-12f;
+        float lo = tlo, hi = thi;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (use[j]) {
+            const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
+            const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
+            const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
+            lo = fmaxf(lo, fminf(t0, t1));
+            hi = fminf(hi, fmaxf(t0, t1));
+          }
+        }
+        const bool hit = lo <= hi && ch[k] != kWorld4Empty;
+        key[k] = hit ? fminf(lo, 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
         hc[k] = ch[k];
       }
       if (STATS) st.v[ST_NODES]++;
@@ -1931,10 +1913,11 @@ __device__ __forceinline__ V3 ld3(const __attribute__((address_space(4))) double
 #define YART_KA_OPAQUE 1
 #endif
 typedef const __attribute__((address_space(4))) RenderArgs* kargs_ptr;
+template <bool OPAQUE>
 __device__ __forceinline__ kargs_ptr kernarg_args() {
   const __attribute__((address_space(4))) char* p =
       (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
+  if (OPAQUE) asm volatile("" : "+s"(p));  // else a fixed address: loads are hoisted as for a plain parameter
   return (kargs_ptr)(p + (kKernargCam - offsetof(RenderArgs, cam)));
 }
 
@@ -2118,12 +2101,13 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
 // DEEP: a mesh deeper than depth 10 (DevScene::deep) — the walk stacks overflow into HBM (OVF above).
 template <bool HAS_MESH, bool BVH, bool STATS, bool DYN, bool EXT, bool DEEP = false>
 __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void k_render(DevScene S, RenderArgs A_) {
-  // The render arguments are read where used, through the opaque kernarg pointer (kernarg_args):
-  // SGPR spills of the chunked list kernel 45 -> 26, world BVH 71 -> 56, mesh 80 -> 60; cornell
-  // 800x800x256 29.16 -> 28.84 ms, the mesh kernels +0.2-0.4 %, random-scene -1 % (noise level;
-  // profiles/r05_ab_covered_ka.log, r05_ab_ka256.log). YART_KA_OPAQUE=0 builds the plain form.
+  // The render arguments are read where used, through the opaque kernarg pointer (kernarg_args), in
+  // the list and mesh kernels: SGPR spills of the chunked list kernel 45 -> 24, mesh 80 -> 54;
+  // cornell 800x800x256 29.16 -> 28.84 ms, the mesh kernels +0.2-0.4 %. The world-BVH kernels keep
+  // the hoisted form (random-scene -1.8 % opaque; profiles/r05_ab_covered_ka.log, r05_ab_ka256.log).
+  // YART_KA_OPAQUE=0 builds the plain form everywhere.
 #if YART_KA_OPAQUE
-#define A (*kernarg_args())
+#define A (*kernarg_args<!BVH>())
 #else
 #define A A_
 #endif
