@@ -464,8 +464,9 @@ def main():
                                      "/ HIP-event kernel time" + ("" if world == 1 else
                                                                    " (shard 0's work / the slowest GPU's kernel time)"),
                     "traffic_source": pmc_source if world == 1 else "not measured for a shard",
-                    # k_render<HAS_MESH, BVH, STATS, DYN, EXT>: the chunked (DYN) list kernel for this frame
-                    "kernel": "k_render<false,false,false,true,false>" if chunked else "k_render<false,false,false,false,false>",
+                    # k_render<HAS_MESH, BVH, STATS, DYN, EXT, DEEP>: the chunked (DYN) list kernel for this frame
+                    "kernel": ("k_render<false,false,false,true,false,false>" if chunked
+                               else "k_render<false,false,false,false,false,false>"),
                     "kernel_ms": round(kern_ms, 3),
                     "accumulate_ms": round(accum_ms, 3) if accum_ms is not None else None,
                     "kernel_ms_source": ("HIP events, 3 frames on one stream after the timed region" if S > 1
