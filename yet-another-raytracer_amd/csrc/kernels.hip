@@ -2234,10 +2234,14 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
         uint32_t jx = x, jy = y;
         if (JOBL) { jx = jl[256]; jy = jl[320]; }
         if (JOBL3) { const uint32_t p = jl[0]; jy = p / W; jx = p - jy * W; }
+        // W - 1 and H - 1 opaque here: hoisted, their f64 conversions held two VGPR pairs through the
+        // whole loop (the mesh kernel spilled them)
+        uint32_t wm1 = W - 1, hm1 = H - 1;
+        asm volatile("" : "+s"(wm1), "+s"(hm1));
         const double tx = (double)jx + gen_f64(g);
-        const double u = tx / (double)(W - 1);
+        const double u = tx / (double)wm1;
         const double ty = (double)jy + gen_f64(g);
-        const double v = 1.0 - ty / (double)(H - 1);
+        const double v = 1.0 - ty / (double)hm1;
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
         ray = camera_ray(*kernarg_camera(), u, v, wl, g, EXT && S.has_time);
         wbin = spectrum_bin(wl);  // the path's reflectance bin (color.rs:276-283), once per sample
