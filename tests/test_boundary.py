@@ -165,6 +165,35 @@ def test_render_multi_async_on_one_device_is_the_render():
     m.close()
 
 
+def test_render_multi_async_evicts_slots_beyond_eight_caller_streams():
+    """a multi handle keeps per-caller-stream slots for at most 8 streams; a 9th and 10th
+    caller stream take over the least recently used slots (their frames drained first), and a reused
+    stream afterwards gets a slot again. Every frame stays bitwise yart_render; yart_multi_query
+    reports the latest frame gathered and unpacked once it is done; the per-device timing covers it."""
+    p = yart.Preset("cornell-box")
+    W, H, spp = 40, 24, 4
+    cam = p.camera(W, H)
+    prm = yart.render_params(W, H, spp, 50)
+    ref = yart.DeviceScene(p).render(cam, prm)
+    m = yart.MultiScene(p, [0])
+    sts = [torch.cuda.Stream() for _ in range(10)]
+    order = list(range(10)) + [0, 3, 9, 1]  # 10 streams (two evictions), then reuse of evicted ones
+    frames = [torch.full((H, W, 3), float("nan"), dtype=torch.float64, device="cuda:0") for _ in order]
+    for k, i in enumerate(order):
+        with torch.cuda.stream(sts[i]):
+            m.render_async(cam, prm, frames[k].data_ptr(), sts[i].cuda_stream)
+    torch.cuda.synchronize()
+    for f in frames:
+        np.testing.assert_array_equal(f.cpu().numpy(), ref)
+    state, unpacked = m.query()
+    assert state == [2] and unpacked == 1
+    r, g, n = m.frame_timing()
+    assert n >= 8 and r > 0  # frames of evicted slots are dropped from the timing
+    dr, dg, dn = m.device_timing()
+    assert len(dr) == 1 and dn == n and dr[0] == pytest.approx(r) and dg[0] > 0
+    m.close()
+
+
 def test_wavefront_frames_back_to_back_on_one_stream():
     """ADVICE r03 (status-ring race): on the wavefront path a pass ends at a data-dependent
     iteration j while iterations j+1 .. j+6 are still queued; the next pass or frame on the same

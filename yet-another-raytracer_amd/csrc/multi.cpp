@@ -186,6 +186,13 @@ struct yart_multi {
     }
     for (int d = 0; d < n && d < (int)devices.size(); ++d) {
       (void)hipSetDevice(devices[(size_t)d]);
+      // the scene's unread frame-timing events of this stream: read and recycled now, or a later
+      // stream that happens to get the same handle would report these frames as its own
+      if ((size_t)d < s.streams.size() && s.streams[(size_t)d] && (size_t)d < scenes.size()) {
+        double r = 0.0, a = 0.0;
+        uint32_t f = 0;
+        (void)yart_frame_timing(scenes[(size_t)d], s.streams[(size_t)d], &r, &a, &f);
+      }
       if ((size_t)d < s.packed.size() && s.packed[(size_t)d]) (void)hipFree(s.packed[(size_t)d]);
       if ((size_t)d < s.gathered.size() && s.gathered[(size_t)d]) (void)hipEventDestroy(s.gathered[(size_t)d]);
       if ((size_t)d < s.rendered.size() && s.rendered[(size_t)d]) (void)hipEventDestroy(s.rendered[(size_t)d]);
