@@ -388,6 +388,7 @@ def main():
     if mode == "ranks":
         with wd.stage("barrier before the timed frames", BASE_DEADLINE_S):
             dist.barrier()
+    gather_evs.clear()  # per-rank gather times: the timed frames (then, with S > 1, the one-stream frames)
     with wd.stage("timed frames", frames_deadline(a.steps), where):
         t0 = time.perf_counter()
         for i in range(a.steps):

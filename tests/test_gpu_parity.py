@@ -330,6 +330,31 @@ def test_world_bvh_4wide_mixed_lists_match_linear_scan(dev, n):
     _hits_equal(h, o, h2, o2)
 
 
+def test_world_bvh_axis_parallel_and_tiny_direction_rays_match_oracle(dev):
+    """The world-BVH walk's slab test leaves an axis unconstrained when the ray's direction has no
+    usable f32 reciprocal there (|d| < 1e-20: zero, denormal-small or tiny components). Rays of the
+    random scene (its 4-wide world BVH) with one or two such components, aimed through the sphere
+    field: closest hits bitwise the oracle's linear HittableList scan."""
+    p = yart.Preset("random-scene")
+    s = yart.DeviceScene(p.desc)
+    assert s.info().world_nodes > 0
+    rng = np.random.default_rng(17)
+    n = 60000
+    o = np.column_stack([rng.uniform(-12, 12, n), rng.uniform(0.05, 1.5, n), rng.uniform(-12, 12, n)])
+    d = rng.normal(size=(n, 3))
+    small = np.array([0.0, -0.0, 1e-30, -1e-25, 5e-324, 1e-21, 2e-20])
+    for j in range(3):  # zero / tiny components on one axis (then two) for blocks of the rays
+        pick = rng.random(n) < 0.35
+        d[pick, j] = rng.choice(small, pick.sum())
+    keep = np.abs(d).max(axis=1) > 1e-3  # at least one usable component
+    o, d = o[keep], d[keep]
+    rays = np.concatenate([o, d, np.full((len(o), 1), 0.001), np.full((len(o), 1), np.inf)], axis=1)
+    h, ob = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, ob, h2, o2)
+
+
 def test_world_bvh_of_a_large_clustered_list_matches_linear_scan(dev):
     """65,536 clustered spheres (oracle_lib.big_sphere_desc), a list whose SAH tree
     the area collapse made too deep for the walk's stack — the scene used to lose its BVH. Now it

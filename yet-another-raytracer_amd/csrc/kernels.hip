@@ -1563,7 +1563,10 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     use[j] = fabsf(d[j]) >= 1.0e-20f;  // smaller: the slab does not constrain t
-    inv[j] = use[j] ? __builtin_amdgcn_rcpf(d[j]) : 0.0f;
+    // an unused axis gets a NaN reciprocal: its t0, t1 are NaN, and fmaxf / fminf (IEEE maxNum /
+    // minNum: the other operand) then leave the interval as it is — the slab unconstrained without
+    // a branch per child and axis
+    inv[j] = use[j] ? __builtin_amdgcn_rcpf(d[j]) : __builtin_nanf("");
   }
   const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
   float tlo = (float)tmin;
@@ -1642,13 +1645,11 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
         float lo = tlo, hi = thi;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          if (use[j]) {
-            const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
-            const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
-            const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
-            lo = fmaxf(lo, fminf(t0, t1));
-            hi = fminf(hi, fmaxf(t0, t1));
-          }
+          const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
+          const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
+          const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
+          lo = fmaxf(lo, fminf(t0, t1));
+          hi = fminf(hi, fmaxf(t0, t1));
         }
         const bool hit = lo <= hi && ch[k] != kWorld4Empty;
         key[k] = hit ? fminf(lo, 3.0e38f) : INFINITY;  // a hit whose entry overflowed stays a hit
