@@ -119,9 +119,11 @@ constexpr uint32_t kWorldHandleFirstMask = 1u << 27;
 static_assert(sizeof(DevWorldNode) == 48, "DevWorldNode must be 48 B");
 // The 4-wide world BVH the device walks (the binary tree above collapsed, two levels per node: each
 // node's four children are the binary tree's nodes two levels down, or fewer where leaves come
-// earlier): per child its f32 box (rounded outward as above), magnitude (margin scale) and handle,
-// laid out per axis so one lane reads a whole node with eight 16-B loads. An empty child slot has
-// the handle kWorld4Empty and is never tested.
+// earlier): per child its f32 box — rounded outward as above and grown by the child's share of the
+// walk's culling margin, mag · 2^-12, rounded outward again, so the walk adds only the ray's share
+// (world_closest_bvh) — its magnitude (kept for the record's 128-B layout; the walk does not read
+// it) and handle, laid out per axis so one lane reads a node with seven 16-B loads. An empty child
+// slot has the handle kWorld4Empty and is never tested.
 struct alignas(16) DevWorldNode4 {
   float bmin[3][4];   // [axis][child]
   float bmax[3][4];

@@ -611,8 +611,8 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
   if (fabsf(hi) < INFINITY) hi = hi + fabsf(hi) * 0x1p-10f;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    if (!(fabsf(d[j]) >= 1.0e-20f)) continue;  // slab unconstrained
-    const float inv = __builtin_amdgcn_rcpf(d[j]);
+    // slab unconstrained: a NaN reciprocal, which fmaxf / fminf (maxNum / minNum) ignore
+    const float inv = fabsf(d[j]) >= 1.0e-20f ? __builtin_amdgcn_rcpf(d[j]) : __builtin_nanf("");
     const float t0 = (bmn[j] - m - o[j]) * inv, t1 = (bmx[j] + m - o[j]) * inv;
     lo = fmaxf(lo, fminf(t0, t1));
     hi = fminf(hi, fmaxf(t0, t1));
@@ -1548,7 +1548,9 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
 // inclusive at t_max), so it returns the minimum r_i, ties going to the LATER object; any visiting
 // order that keeps (min t, max index) returns the same winner, and the record is then rebuilt from
 // it as before. Node culling is an f32 slab test against the box grown by m = 2^-12 (node
-// magnitude + |origin|) — f32 rounding (~1e-7 relative) stays far inside m — over [t_min, closest]
+// magnitude + |origin|; the node's share is stored in the box, the ray's is added per walk, r05:
+// random-scene +4.4-5.8 %, profiles/r05_ab_world_fma_slab.log) — f32 rounding (~1e-7 relative,
+// the fma's and the per-ray constants' included) stays far inside m — over [t_min, closest]
 // widened by 2^-10, so it never drops a node holding a hit the scan would accept (ties included).
 // Non-finite rays take the list walk.
 template <bool STATS>
@@ -1569,6 +1571,16 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
     inv[j] = use[j] ? __builtin_amdgcn_rcpf(d[j]) : __builtin_nanf("");
   }
   const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
+  // child boxes come grown by their own margin (mag 2^-12, DevWorldNode4); the ray's share, O 2^-12,
+  // goes into per-ray constants so that each slab bound is one fma: t0 = (bl - mr - o) inv =
+  // fma(bl, inv, -(o + mr) inv), t1 = fma(bh, inv, (mr - o) inv). A ray whose constants could
+  // overflow (|o| |1/d| near the f32 range) takes the list walk.
+  const float mr = O * 0x1p-12f;
+  const float imax = fmaxf(fmaxf(fabsf(inv[0]), fabsf(inv[1])), fabsf(inv[2]));
+  if (!((O + mr) * imax <= 1.0e37f)) return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
+  float ca[3], cb[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) { ca[j] = -((o[j] + mr) * inv[j]); cb[j] = (mr - o[j]) * inv[j]; }
   float tlo = (float)tmin;
   tlo = tlo - fabsf(tlo) * 0x1p-10f;
   bool found = false;
@@ -1631,8 +1643,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       float4 bmn[3], bmx[3];
       bmn[0] = ld4(N, 0); bmn[1] = ld4(N, 1); bmn[2] = ld4(N, 2);
       bmx[0] = ld4(N, 3); bmx[1] = ld4(N, 4); bmx[2] = ld4(N, 5);
-      const float4 mg = ld4(N, 6), hd = ld4(N, 7);
-      const float mk[4] = {mg.x, mg.y, mg.z, mg.w};
+      const float4 hd = ld4(N, 7);
       const uint32_t ch[4] = {__float_as_uint(hd.x), __float_as_uint(hd.y), __float_as_uint(hd.z), __float_as_uint(hd.w)};
       // per child: the binary tree's test of that node (the same expression on the same box). (A
       // packed-f32 form, two children per v_pk_add_f32 / v_pk_mul_f32, lost 3 % on the random scene
@@ -1641,13 +1652,12 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
       uint32_t hc[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float m = (mk[k] + O) * 0x1p-12f;
         float lo = tlo, hi = thi;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const float bl = k == 0 ? bmn[j].x : k == 1 ? bmn[j].y : k == 2 ? bmn[j].z : bmn[j].w;
           const float bh = k == 0 ? bmx[j].x : k == 1 ? bmx[j].y : k == 2 ? bmx[j].z : bmx[j].w;
-          const float t0 = (bl - m - o[j]) * inv[j], t1 = (bh + m - o[j]) * inv[j];
+          const float t0 = __builtin_fmaf(bl, inv[j], ca[j]), t1 = __builtin_fmaf(bh, inv[j], cb[j]);
           lo = fmaxf(lo, fminf(t0, t1));
           hi = fminf(hi, fmaxf(t0, t1));
         }

@@ -238,7 +238,9 @@ bool collapse4(BuiltWorld& out, bool two_level) {
         continue;
       }
       const DevWorldNode& c = out.nodes[kids[k]];
-      for (int a = 0; a < 3; ++a) { q.bmin[a][k] = c.bmin[a]; q.bmax[a][k] = c.bmax[a]; }
+      // grown by the child's share of the walk's margin (mag 2^-12, world_closest_bvh), rounded outward
+      const double gm = (double)c.mag * 0x1p-12;
+      for (int a = 0; a < 3; ++a) { q.bmin[a][k] = down((double)c.bmin[a] - gm); q.bmax[a][k] = up((double)c.bmax[a] + gm); }
       q.mag[k] = c.mag;
       if (c.count) {
         q.handle[k] = c.pad[1];  // a leaf
