@@ -423,7 +423,8 @@ int yart_qbvh_build(const float* positions, const double* normals, uint32_t n_tr
  * tree the device walks, built exactly as yart_scene_create builds them (whatever the object count;
  * built = 0 when some object has no box: meshes, media, moving spheres), then the 4-wide tree's
  * structural check (world_bvh.cpp check_world4: every object in exactly one leaf, every child box
- * holding the objects below it, depth within the walk's stack; valid = 1, or the reason in
+ * holding the objects below it grown by the child's culling margin (magnitude 2^-12, the magnitude
+ * bounding its coordinates), depth within the walk's stack; valid = 1, or the reason in
  * yart_last_error). digest: FNV-1a 64 over the 4-wide nodes, leaf slots and sphere records. */
 typedef struct yart_world_bvh_info {
   uint32_t built, nodes, depth, nodes4, depth4, valid;

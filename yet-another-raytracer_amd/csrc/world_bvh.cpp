@@ -370,6 +370,13 @@ bool check_world4(const std::vector<DevObject>& objs, const BuiltWorld& w, std::
         if (!world_bounds(objs[i], lo, hi)) { err = "object without a box in the tree"; return false; }
         for (int a = 0; a < 3; ++a)
           if (!((double)q.bmin[a][k] <= lo[a] && hi[a] <= (double)q.bmax[a][k])) { err = "child box does not hold an object below it"; return false; }
+        // what world_closest_bvh's culling margin assumes: the magnitude bounds the child's
+        // coordinates, and the stored box holds the objects grown by the child's share, mag 2^-12
+        const double gm = (double)q.mag[k] * 0x1p-12;
+        for (int a = 0; a < 3; ++a) {
+          if (!((double)q.mag[k] >= std::fabs(lo[a]) && (double)q.mag[k] >= std::fabs(hi[a]))) { err = "child magnitude below its coordinates"; return false; }
+          if (!((double)q.bmin[a][k] <= lo[a] - gm && hi[a] + gm <= (double)q.bmax[a][k])) { err = "child box not grown by its margin"; return false; }
+        }
       }
       if (count) {
         const bool spheres = ((h >> 27) & 1u) != 0;
