@@ -355,6 +355,38 @@ def test_world_bvh_axis_parallel_and_tiny_direction_rays_match_oracle(dev):
     _hits_equal(h, ob, h2, o2)
 
 
+def test_world_bvh_far_origins_and_near_overflow_slab_constants_match_oracle(dev):
+    """The walk's per-ray slab constants, -(o + m)/d and (m - o)/d, reach |o| |1/d|: a ray whose
+    constants could overflow f32 (|o| |1/d| > 1e37) takes the list walk, one below that walks the
+    tree on huge constants. Rays from origins 10^3 .. 10^30 away, aimed at points of the sphere
+    field, a third of them with one direction component cut to 1e-19 .. 1e-12 (the target kept on
+    the ray): both sides of the cut-off, bitwise the oracle's linear HittableList scan."""
+    p = yart.Preset("random-scene")
+    s = yart.DeviceScene(p.desc)
+    assert s.info().world_nodes > 0
+    rng = np.random.default_rng(23)
+    n = 40000
+    tgt = np.column_stack([rng.uniform(-11, 11, n), rng.uniform(0.0, 1.2, n), rng.uniform(-11, 11, n)])
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    far = 10.0 ** rng.uniform(3, 30, n)
+    d = u * far[:, None]
+    o = tgt - d
+    pick = rng.random(n) < 0.35
+    ax = rng.integers(0, 3, n)
+    tiny = rng.choice([1e-19, -3e-18, 5e-16, -1e-12], n)
+    rows = np.nonzero(pick)[0]
+    d[rows, ax[rows]] = tiny[rows]
+    o[rows, ax[rows]] = tgt[rows, ax[rows]] - tiny[rows]
+    big = np.abs(o).max(axis=1) / np.maximum(np.abs(d), 1e-20).min(axis=1)
+    assert (big > 1e37).sum() > 1000 and ((big < 1e37) & pick).sum() > 1000  # both walks exercised
+    rays = np.concatenate([o, d, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+    h, ob = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, ob, h2, o2)
+
+
 def test_world_bvh_of_a_large_clustered_list_matches_linear_scan(dev):
     """65,536 clustered spheres (oracle_lib.big_sphere_desc), a list whose SAH tree
     the area collapse made too deep for the walk's stack — the scene used to lose its BVH. Now it
