@@ -136,11 +136,14 @@ __device__ __forceinline__ bool flagged(const Ieee&) { return false; }
 // Policy per kernel, bitwise either way (the flagged re-run replays the draws on Ieee). r02
 // measurement after the register-liveness work, the Fast policy in every kernel vs Ieee in every
 // kernel: cornell (list, no EXT) 4,814 vs 4,716 Msamples/s, random-scene (world BVH) 1,464 vs
-// 1,514, david (mesh) 243.4 vs 243.3. So Fast runs where it wins, the plain list kernel; the
-// others keep Ieee (the second copy of the block costs them registers).
+// 1,514, david (mesh) 243.4 vs 243.3. So Fast ran where it won, the plain list kernel, and the
+// others kept Ieee (the second copy of the block costs them registers). Re-measured in r05 on the
+// world-BVH kernel after its walk changes: +0.2..+2.1 % over five same-box runs
+// (profiles/r05_ab_bvh_fast_policy_*.log), so the world-BVH kernel runs Fast too; the mesh and EXT
+// kernels keep Ieee.
 template <bool HAS_MESH, bool BVH, bool EXT>
 struct MathPolicy {
-  typedef typename std::conditional<!HAS_MESH && !BVH && !EXT, Fast, Ieee>::type type;
+  typedef typename std::conditional<!HAS_MESH && !EXT, Fast, Ieee>::type type;
 };
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
