@@ -9,6 +9,9 @@
 #include <cmath>
 #include <cstring>
 #include <vector>
+#ifdef YART_WALK_TREE_STATS
+#include <cstdio>
+#endif
 
 #include "bvh_build.h"
 
@@ -43,12 +46,30 @@ uint32_t min_levels(size_t n) {
   return l;
 }
 
+// The SAH's count term: the quad steps a part's leaves take, ceil(n / 4), not its triangle count.
+// A leaf step costs the walk one round for its quad whether the leaf holds 1 or 4 triangles, so
+// cuts at multiples of 4 are what saves rounds (r05: leaves 2.05 -> 2.55 triangles, quad steps per
+// ray through the root by surface area 18.24 -> 17.77 on david; bunny +1.0 %, david +1.9 / +2.4 %,
+// same box, bitwise: profiles/r05_ab_walk_tree_quad_sah.log). YART_WALK_LEAF_QUANT=1 (make variant
+// DEFS=...) builds the r03-r04 tree.
+#ifndef YART_WALK_LEAF_QUANT
+#define YART_WALK_LEAF_QUANT 4
+#endif
+double wcount(size_t n) { return (double)((n + YART_WALK_LEAF_QUANT - 1) / YART_WALK_LEAF_QUANT); }
+
 struct WalkBuilder {
   BuiltMesh& m;
   std::vector<WItem> items;
   uint32_t n_tris = 0, max_depth = 10, depth = 0, next_rec = 0;
+#ifdef YART_WALK_TREE_STATS
+  // surface-area sums (study builds, make variant DEFS=-DYART_WALK_TREE_STATS): inner nodes, leaves,
+  // leaves x triangles, and the leaf count
+  double s_inner = 0.0, s_leaf = 0.0, s_tris = 0.0;
+  size_t n_leaves = 0;
+#endif
   // SAH bins per axis; the greedy 4-way expansion splits the part of largest area x count next
-  // (16 / 32 / 64 bins and count- or area-only picks were within +-2 %)
+  // (16 / 32 / 64 bins and count- or area-only picks were within +-2 %; r05: an exact
+  // sweep below 64 / 256 triangles and picking by the SAH gain moved the surface-area estimate < 0.5 %)
   static constexpr int kBins = 32;
 
   // Binned SAH cut of items[b, e) (n >= 2): returns the cut position in (b, e), items partitioned.
@@ -87,7 +108,7 @@ struct WalkBuilder {
         left.grow(bb[k]);
         ln += cnt[k];
         if (ln == 0 || rc[k + 1] == 0) continue;
-        const double cost = left.area() * (double)ln + right[k + 1].area() * (double)rc[k + 1];
+        const double cost = left.area() * wcount(ln) + right[k + 1].area() * wcount(rc[k + 1]);
         if (cost < best) { best = cost; best_axis = axis; best_bin = k; }
       }
     }
@@ -135,6 +156,10 @@ struct WalkBuilder {
     const size_t n = e - b;
     box_out = Box3();
     for (size_t i = b; i < e; ++i) box_out.grow(items[i]);
+#ifdef YART_WALK_TREE_STATS
+    if (n <= 4) { s_leaf += box_out.area(); s_tris += box_out.area() * (double)n; ++n_leaves; }
+    else s_inner += box_out.area();
+#endif
     if (n <= 4) return leaf(b, e);
     depth = std::max(depth, level + 1);
     size_t cut[5];
@@ -210,6 +235,12 @@ void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
   m.walk_nodes = (uint32_t)m.nodes.size() - m.ref_nodes;
   m.walk_depth = w.depth;
   m.walk_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+#ifdef YART_WALK_TREE_STATS
+  // expected visits per ray through the root box, by surface area (no occlusion, no culling)
+  const double ar = root_box.area();
+  std::fprintf(stderr, "walk-tree n %u nodes %u depth %u inner %.3f leaf %.3f tris %.3f fill %.3f\n", w.n_tris,
+               m.walk_nodes, w.depth, w.s_inner / ar, w.s_leaf / ar, w.s_tris / ar, (double)w.n_tris / (double)w.n_leaves);
+#endif
 }
 
 bool check_walk_tree(const BuiltMesh& m, uint32_t max_depth) {
