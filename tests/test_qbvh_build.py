@@ -1,6 +1,7 @@
 """The host QBVH builder (L4QBVH::new, qbvh.rs:252-361) without a GPU: the threaded build is
 byte-identical to the sequential one, the reference's shape for the repo's meshes, and the
 exposure to Rust's sort_unstable_by tie freedom (qbvh.rs:679-685) counted and pinned."""
+import numpy as np
 import pytest
 
 import yart
@@ -65,6 +66,31 @@ def test_walk_tree_structure(meshes, name):
     assert w["nodes"] == MESHES[name][1]  # the reference tree's shape is unchanged
     assert yart.qbvh_build(pos, nrm, yart.QBVH_WALK | yart.QBVH_SERIAL)["digest"] == w["digest"]
     assert yart.qbvh_build(pos, nrm)["digest"] != w["digest"]
+
+
+@pytest.mark.parametrize("n,layout", [(5, "soup"), (6, "soup"), (8, "soup"), (17, "soup"), (65, "soup"),
+                                      (1000, "soup"), (30000, "soup"), (3000, "geometric"), (600, "coincident")])
+def test_walk_tree_of_triangle_soups(n, layout):
+    """r05: the walk tree is collapsed from a binary SAH tree by dynamic programming (walk_tree.cpp
+    build_dp: four subtrees per inner node, leaves of <= 4 triangles, no path deeper than the
+    stack allows), with the greedy builder as fallback. Random soups of awkward sizes, a geometric
+    progression of triangle positions (the most unbalanced cuts) and many coincident triangles:
+    the structural check passes (every triangle in one walk leaf, boxes nested and non-empty, four
+    children per inner node, depth within the 32-slot stack) and the build is deterministic."""
+    rng = np.random.default_rng(n)
+    if layout == "soup":
+        c = rng.uniform(-50, 50, (n, 1, 3))
+    elif layout == "geometric":  # positions 1.1^k along x: every SAH cut isolates the far end
+        c = np.zeros((n, 1, 3))
+        c[:, 0, 0] = 1.1 ** np.arange(n) % 1e30
+    else:
+        c = np.zeros((n, 1, 3))
+    pos = (c + rng.normal(0, 0.3, (n, 3, 3))).astype(np.float32).reshape(n, 9)
+    nrm = np.zeros((n, 9))
+    w = yart.qbvh_build(pos, nrm, yart.QBVH_WALK)
+    assert w["walk_valid"] == 1
+    assert w["walk_nodes"] > 0 and 3 * w["walk_depth"] + 1 <= 32
+    assert yart.qbvh_build(pos, nrm, yart.QBVH_WALK)["digest"] == w["digest"]
 
 
 @pytest.mark.parametrize("scene", ["random-scene", "cornell-box", "three-spheres", "two-spheres"])

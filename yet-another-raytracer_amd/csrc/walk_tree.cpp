@@ -55,6 +55,16 @@ uint32_t min_levels(size_t n) {
 #ifndef YART_WALK_LEAF_QUANT
 #define YART_WALK_LEAF_QUANT 4
 #endif
+// The 4-wide tree from a binary SAH tree by dynamic programming (r05, the default; 0: the greedy
+// 4-way expansion of r03-r04), for meshes of at most kDpMaxTris triangles (its tables take ~660 B
+// per triangle); larger meshes, or a mesh whose tree cannot fit the depth bound, take the greedy one.
+#ifndef YART_WALK_DP
+#define YART_WALK_DP 1
+#endif
+#ifndef YART_WALK_DP_CL
+#define YART_WALK_DP_CL 1.0  // a leaf step's cost against an inner node step's
+#endif
+constexpr uint32_t kDpMaxTris = 1u << 17;
 double wcount(size_t n) { return (double)((n + YART_WALK_LEAF_QUANT - 1) / YART_WALK_LEAF_QUANT); }
 
 struct WalkBuilder {
@@ -152,6 +162,105 @@ struct WalkBuilder {
     return (1u << 31) | ((uint32_t)(e - b) << 27) | first;
   }
 
+#if YART_WALK_DP
+  // A binary SAH tree (the same binned cut) down to single triangles, collapsed into the 4-wide tree
+  // by dynamic programming over the expected quad steps (surface area per node visit): each inner
+  // node takes exactly four subtrees of its binary node, a leaf any subtree of <= 4 triangles, and
+  // no path has more than max_depth inner nodes. r05: steps per ray through the root by surface
+  // area 17.77 -> 17.16 on david (18.13 -> 17.64 sycee), leaves 2.55 -> 3.08 triangles; same box,
+  // bitwise, david +0.9 .. +1.3 %, bunny +0.1 / +0.9 % (profiles/r05_ab_walk_tree_dp.log).
+  struct BNode { Box3 box; size_t b, e; int l = -1, r = -1; };
+  std::vector<BNode> bn;
+  // memo per (node, remaining inner levels d): c1 as one child, dd as exactly i subtrees
+  std::vector<float> c1, dd;
+  std::vector<signed char> c1leaf, dj;
+  int DL = 0;  // max_depth: the levels the root may use
+  size_t ix(int id, int d) const { return (size_t)id * (size_t)(DL + 1) + (size_t)d; }
+  // (recursion bounded: a node cut off at level 96 with more than 4 triangles has no 4-wide form,
+  // so the DP finds no tree and the greedy builder takes over)
+  int bbuild(size_t b, size_t e, int level) {
+    BNode nd; nd.b = b; nd.e = e;
+    for (size_t i = b; i < e; ++i) nd.box.grow(items[i]);
+    const int id = (int)bn.size();
+    bn.push_back(nd);
+    if (e - b <= 1 || level >= 96) return id;
+    const size_t c = split(b, e);
+    const int l = bbuild(b, c, level + 1), r = bbuild(c, e, level + 1);
+    bn[id].l = l; bn[id].r = r;
+    return id;
+  }
+  float D(int id, int i, int d) {
+    float& v = dd[ix(id, d) * 5 + i];
+    if (v == v) return v;  // memo (NaN = unset)
+    if (i == 1) { v = C1(id, d); return v; }
+    const BNode& nd = bn[id];
+    v = INFINITY;
+    if (nd.l < 0) return v;
+    for (int j = 1; j < i; ++j) {
+      const float c = D(nd.l, j, d) + D(nd.r, i - j, d);
+      if (c < v) { v = c; dj[ix(id, d) * 5 + i] = (signed char)j; }
+    }
+    return v;
+  }
+  float C1(int id, int d) {
+    float& v = c1[ix(id, d)];
+    if (v == v) return v;
+    const BNode& nd = bn[id];
+    const size_t n = nd.e - nd.b;
+    v = INFINITY;
+    if (n <= 4) { v = (float)(nd.box.area() * YART_WALK_DP_CL); c1leaf[ix(id, d)] = 1; }
+    if (n >= 4 && nd.l >= 0 && d >= 1) {
+      const float c = (float)nd.box.area() + D(id, 4, d - 1);
+      if (c < v) { v = c; c1leaf[ix(id, d)] = 0; }
+    }
+    return v;
+  }
+  void gather(int id, int i, int d, std::vector<int>& out) {
+    if (i == 1) { out.push_back(id); return; }
+    const int j = dj[ix(id, d) * 5 + i];
+    gather(bn[id].l, j, d, out);
+    gather(bn[id].r, i - j, d, out);
+  }
+  uint32_t emit(int id, int d, uint32_t level, Box3& box_out) {
+    const BNode& nd = bn[id];
+    box_out = nd.box;
+    const bool lf = c1leaf[ix(id, d)] != 0;
+#ifdef YART_WALK_TREE_STATS
+    if (lf) { s_leaf += box_out.area(); s_tris += box_out.area() * (double)(nd.e - nd.b); ++n_leaves; }
+    else s_inner += box_out.area();
+#endif
+    if (lf) return leaf(nd.b, nd.e);
+    depth = std::max(depth, level + 1);
+    std::vector<int> sub;
+    gather(id, 4, d - 1, sub);
+    Box3 cb[4];
+    uint32_t ch[4];
+    for (int q = 0; q < 4; ++q) ch[q] = emit(sub[q], d - 1, level + 1, cb[q]);
+    DevNode node{};
+    for (int q = 0; q < 4; ++q) {
+      node.lo[q][0] = cb[q].lo[0]; node.lo[q][1] = cb[q].hi[0]; node.lo[q][2] = cb[q].lo[1]; node.lo[q][3] = cb[q].hi[1];
+      node.hi[q][0] = cb[q].lo[2]; node.hi[q][1] = cb[q].hi[2];
+      std::memcpy(&node.hi[q][2], &ch[q], 4);
+      const uint32_t zero = 0;
+      std::memcpy(&node.hi[q][3], &zero, 4);
+    }
+    m.nodes.push_back(node);
+    return (uint32_t)m.nodes.size() - 1;
+  }
+  // The tree's root, or false when no tree fits max_depth (nothing emitted then).
+  bool build_dp(Box3& root_box, uint32_t& root_out) {
+    DL = (int)max_depth;
+    const int root = bbuild(0, items.size(), 0);
+    c1.assign(bn.size() * (size_t)(DL + 1), NAN); dd.assign(bn.size() * (size_t)(DL + 1) * 5, NAN);
+    c1leaf.assign(bn.size() * (size_t)(DL + 1), 0); dj.assign(bn.size() * (size_t)(DL + 1) * 5, 0);
+    const bool ok = C1(root, DL) < INFINITY;
+    if (ok) root_out = emit(root, DL, 0, root_box);
+    std::vector<BNode>().swap(bn);
+    std::vector<float>().swap(c1); std::vector<float>().swap(dd);
+    std::vector<signed char>().swap(c1leaf); std::vector<signed char>().swap(dj);
+    return ok;
+  }
+#endif
   uint32_t build(size_t b, size_t e, uint32_t level, Box3& box_out) {
     const size_t n = e - b;
     box_out = Box3();
@@ -226,7 +335,12 @@ void build_walk_tree(BuiltMesh& m, uint32_t max_depth) {
   }
   m.leaves.resize(2 * m.leaves.size());
   Box3 root_box;
-  const uint32_t root = w.build(0, w.n_tris, 0, root_box);
+  uint32_t root = 0;
+  bool built = false;
+#if YART_WALK_DP
+  if (w.n_tris <= kDpMaxTris) built = w.build_dp(root_box, root);
+#endif
+  if (!built) root = w.build(0, w.n_tris, 0, root_box);
   if (root >> 31) {  // a single leaf (<= 4 triangles): keep walking the reference tree
     m.leaves.resize(m.leaves.size() / 2);
     return;
