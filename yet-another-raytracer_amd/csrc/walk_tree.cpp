@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <future>
 #include <vector>
 #ifdef YART_WALK_TREE_STATS
 #include <cstdio>
@@ -56,7 +57,7 @@ uint32_t min_levels(size_t n) {
 #define YART_WALK_LEAF_QUANT 4
 #endif
 // The 4-wide tree from a binary SAH tree by dynamic programming (r05, the default; 0: the greedy
-// 4-way expansion of r03-r04), for meshes of at most kDpMaxTris triangles (its tables take ~660 B
+// 4-way expansion of r03-r04), for meshes of at most kDpMaxTris triangles (its tables take ~100 B
 // per triangle); larger meshes, or a mesh whose tree cannot fit the depth bound, take the greedy one.
 #ifndef YART_WALK_DP
 #define YART_WALK_DP 1
@@ -169,40 +170,65 @@ struct WalkBuilder {
   // no path has more than max_depth inner nodes. r05: steps per ray through the root by surface
   // area 17.77 -> 17.16 on david (18.13 -> 17.64 sycee), leaves 2.55 -> 3.08 triangles; same box,
   // bitwise, david +0.9 .. +1.3 %, bunny +0.1 / +0.9 % (profiles/r05_ab_walk_tree_dp.log).
-  struct BNode { Box3 box; size_t b, e; int l = -1, r = -1; };
+  struct BNode { Box3 box; size_t b, e; int l = -1, r = -1, h = 0; };  // h: binary height below
   std::vector<BNode> bn;
-  // memo per (node, remaining inner levels d): c1 as one child, dd as exactly i subtrees
+  // memo per (node, remaining inner levels d <= min(h, max_depth)): a 4-wide tree cut from a binary
+  // subtree of height h is never deeper than h, so a larger d is the same as d = h
   std::vector<float> c1, dd;
   std::vector<signed char> c1leaf, dj;
-  int DL = 0;  // max_depth: the levels the root may use
-  size_t ix(int id, int d) const { return (size_t)id * (size_t)(DL + 1) + (size_t)d; }
+  std::vector<size_t> off;  // per node: first memo slot
+  int DL = 0;               // max_depth: the levels the root may use
+  int clampd(int id, int d) const { return std::min(d, bn[id].h); }
+  size_t ix(int id, int d) const { return off[id] + (size_t)d; }
   // (recursion bounded: a node cut off at level 96 with more than 4 triangles has no 4-wide form,
-  // so the DP finds no tree and the greedy builder takes over)
-  int bbuild(size_t b, size_t e, int level) {
+  // so the DP finds no tree and the greedy builder takes over). The top levels' subtrees (disjoint
+  // item ranges) build concurrently into their own node lists, appended in preorder: the nodes and
+  // their numbering are the serial build's.
+  int bbuild(std::vector<BNode>& out, size_t b, size_t e, int level) {
     BNode nd; nd.b = b; nd.e = e;
-    for (size_t i = b; i < e; ++i) nd.box.grow(items[i]);
-    const int id = (int)bn.size();
-    bn.push_back(nd);
-    if (e - b <= 1 || level >= 96) return id;
+    const int id = (int)out.size();
+    out.push_back(nd);
+    if (e - b <= 1 || level >= 96) {
+      for (size_t i = b; i < e; ++i) out[id].box.grow(items[i]);
+      return id;
+    }
     const size_t c = split(b, e);
-    const int l = bbuild(b, c, level + 1), r = bbuild(c, e, level + 1);
-    bn[id].l = l; bn[id].r = r;
+    int l, r;
+    if (e - b >= 16384 && level < 3) {
+      std::vector<BNode> lv, rv;
+      auto right = std::async(std::launch::async, [&] { bbuild(rv, c, e, level + 1); });
+      bbuild(lv, b, c, level + 1);
+      right.get();
+      l = (int)out.size();
+      for (BNode x : lv) { if (x.l >= 0) { x.l += l; x.r += l; } out.push_back(x); }
+      r = (int)out.size();
+      for (BNode x : rv) { if (x.l >= 0) { x.l += r; x.r += r; } out.push_back(x); }
+    } else {
+      l = bbuild(out, b, c, level + 1);
+      r = bbuild(out, c, e, level + 1);
+    }
+    BNode& me = out[id];
+    me.l = l; me.r = r;
+    me.h = 1 + std::max(out[l].h, out[r].h);
+    me.box = out[l].box;
+    me.box.grow(out[r].box);
     return id;
   }
   float D(int id, int i, int d) {
-    float& v = dd[ix(id, d) * 5 + i];
+    d = clampd(id, d);
+    float& v = dd[ix(id, d) * 3 + (i - 2)];
     if (v == v) return v;  // memo (NaN = unset)
-    if (i == 1) { v = C1(id, d); return v; }
     const BNode& nd = bn[id];
     v = INFINITY;
     if (nd.l < 0) return v;
     for (int j = 1; j < i; ++j) {
-      const float c = D(nd.l, j, d) + D(nd.r, i - j, d);
-      if (c < v) { v = c; dj[ix(id, d) * 5 + i] = (signed char)j; }
+      const float c = (j == 1 ? C1(nd.l, d) : D(nd.l, j, d)) + (i - j == 1 ? C1(nd.r, d) : D(nd.r, i - j, d));
+      if (c < v) { v = c; dj[ix(id, d) * 3 + (i - 2)] = (signed char)j; }
     }
     return v;
   }
   float C1(int id, int d) {
+    d = clampd(id, d);
     float& v = c1[ix(id, d)];
     if (v == v) return v;
     const BNode& nd = bn[id];
@@ -217,13 +243,15 @@ struct WalkBuilder {
   }
   void gather(int id, int i, int d, std::vector<int>& out) {
     if (i == 1) { out.push_back(id); return; }
-    const int j = dj[ix(id, d) * 5 + i];
+    d = clampd(id, d);
+    const int j = dj[ix(id, d) * 3 + (i - 2)];
     gather(bn[id].l, j, d, out);
     gather(bn[id].r, i - j, d, out);
   }
   uint32_t emit(int id, int d, uint32_t level, Box3& box_out) {
     const BNode& nd = bn[id];
     box_out = nd.box;
+    d = clampd(id, d);
     const bool lf = c1leaf[ix(id, d)] != 0;
 #ifdef YART_WALK_TREE_STATS
     if (lf) { s_leaf += box_out.area(); s_tris += box_out.area() * (double)(nd.e - nd.b); ++n_leaves; }
@@ -250,14 +278,18 @@ struct WalkBuilder {
   // The tree's root, or false when no tree fits max_depth (nothing emitted then).
   bool build_dp(Box3& root_box, uint32_t& root_out) {
     DL = (int)max_depth;
-    const int root = bbuild(0, items.size(), 0);
-    c1.assign(bn.size() * (size_t)(DL + 1), NAN); dd.assign(bn.size() * (size_t)(DL + 1) * 5, NAN);
-    c1leaf.assign(bn.size() * (size_t)(DL + 1), 0); dj.assign(bn.size() * (size_t)(DL + 1) * 5, 0);
+    const int root = bbuild(bn, 0, items.size(), 0);
+    off.resize(bn.size() + 1);
+    off[0] = 0;
+    for (size_t k = 0; k < bn.size(); ++k) off[k + 1] = off[k] + (size_t)std::min(bn[k].h, DL) + 1;
+    c1.assign(off.back(), NAN); dd.assign(off.back() * 3, NAN);
+    c1leaf.assign(off.back(), 0); dj.assign(off.back() * 3, 0);
     const bool ok = C1(root, DL) < INFINITY;
     if (ok) root_out = emit(root, DL, 0, root_box);
     std::vector<BNode>().swap(bn);
     std::vector<float>().swap(c1); std::vector<float>().swap(dd);
     std::vector<signed char>().swap(c1leaf); std::vector<signed char>().swap(dj);
+    std::vector<size_t>().swap(off);
     return ok;
   }
 #endif
