@@ -64,6 +64,9 @@ def test_walk_tree_structure(meshes, name):
     assert w["walk_valid"] == 1
     assert w["walk_nodes"] > 0 and 3 * w["walk_depth"] + 1 <= 32
     assert w["nodes"] == MESHES[name][1]  # the reference tree's shape is unchanged
+    # r05's tree (quad-step SAH, depth-bounded DP collapse): a silent fall back to the greedy
+    # builder (david 6,111 nodes, depth 9) or the r04 tree (7,598) shows here
+    assert (w["walk_nodes"], w["walk_depth"]) == {"cube": (1, 1), "david": (5054, 10), "sycee": (3416, 10)}[name]
     assert yart.qbvh_build(pos, nrm, yart.QBVH_WALK | yart.QBVH_SERIAL)["digest"] == w["digest"]
     assert yart.qbvh_build(pos, nrm)["digest"] != w["digest"]
 
