@@ -730,6 +730,44 @@ def test_mesh_instances_at_random_angles_match_oracle(dev, repo):
                                   O.OracleScene(d).render(cam, yart.render_params(W, H, spp, 16)))
 
 
+@pytest.mark.parametrize("n,layout", [(17, "soup"), (65, "soup"), (1000, "soup"), (30000, "soup"),
+                                      (3000, "geometric"), (600, "coincident")])
+def test_walk_tree_of_triangle_soups_matches_oracle(dev, n, layout):
+    """r05: the front-to-back walk's tree is collapsed from a binary SAH tree by dynamic programming
+    (walk_tree.cpp), with unusual shapes on unusual inputs: random soups of awkward sizes, triangles
+    along a geometric progression (the most unbalanced cuts) and coincident triangles (every cut a
+    tie). Closest hits of rays aimed at the triangles, bitwise the oracle's (the reference's walk)."""
+    rng = np.random.default_rng(1000 + n)
+    if layout == "soup":
+        c = rng.uniform(-5, 5, (n, 1, 3))
+    elif layout == "geometric":
+        c = np.zeros((n, 1, 3))
+        c[:, 0, 0] = 1.01 ** np.arange(n) - 1.0
+    else:
+        c = np.zeros((n, 1, 3))
+    v = c + rng.normal(0, 0.3, (n, 3, 3))
+    pos = v.astype(np.float32).reshape(n, 9)
+    pv = pos.reshape(n, 3, 3).astype(np.float64)
+    fn = np.cross(pv[:, 1] - pv[:, 0], pv[:, 2] - pv[:, 0])
+    fn /= np.maximum(np.linalg.norm(fn, axis=1), 1e-30)[:, None]
+    nrm = np.repeat(fn[:, None, :], 3, axis=1).reshape(n, 9)
+    b = O.DescBuilder(background=(0.5, 0.6, 0.7))
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.6, 0.6, 0.6)))
+    b.mesh(pos, nrm)
+    b.obj(abi.PRIM_MESH, m, mesh=0)
+    d = b.desc()
+    k = 20000
+    cen = pv.mean(axis=1)
+    org = cen[rng.integers(0, n, k)] + rng.normal(0, 3.0, (k, 3))
+    tgt = cen[rng.integers(0, n, k)] + rng.normal(0, 0.05, (k, 3))
+    rays = np.column_stack([org, tgt - org, np.full(k, 0.001), np.full(k, np.inf)])
+    s = yart.DeviceScene(d)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, o, h2, o2)
+
+
 @pytest.mark.parametrize("wavefront", [0, 1])
 def test_deep_mesh_walks_with_the_references_64_slot_stack(dev, wavefront):
     """A mesh deeper than depth 10 (VERDICT r02 Missing #3, r04 Missing #3): the reference walks it
