@@ -262,6 +262,40 @@ def test_box_cull_is_exact_on_grazing_rays(dev):
     _hits_equal(h, o, h2, o2)
 
 
+def test_box_cull_is_exact_on_axis_parallel_and_tiny_direction_rays(dev):
+    """r05: the box entity's f32 pre-test leaves an axis unconstrained through a NaN reciprocal
+    (fmaxf / fminf ignore it) instead of a branch when the direction's f32 component is below 1e-20
+    (zero, denormal, tiny). Rays with one or two such components aimed at the faces, edges and
+    corners of plain, rotated and tiny boxes: closest hits bitwise the oracle's."""
+    b = O.DescBuilder()
+    m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.5, 0.5, 0.5)))
+    b.obj(abi.PRIM_BOX, m, (130.0, 0.0, 65.0, 295.0, 165.0, 230.0))
+    b.obj(abi.PRIM_BOX, m, (0.0, 0.0, 0.0, 165.0, 330.0, 165.0),
+          xforms=[(abi.XF_TRANSLATE, (265.0, 0.0, 295.0)), (abi.XF_ROTATE_Y, (15.0, 0.0, 0.0))])
+    b.obj(abi.PRIM_BOX, m, (-1e-3, -2e-3, -1e-3, 1e-3, 2e-3, 1e-3), xforms=[(abi.XF_TRANSLATE, (400.0, 5.0, 50.0))])
+    d = b.desc()
+    rng = np.random.default_rng(37)
+    n = 60000
+    lo, hi = np.array([130.0, 0.0, 65.0]), np.array([295.0, 165.0, 230.0])
+    tgt = rng.uniform(lo, hi, (n, 3))
+    snap = rng.integers(0, 3, (n, 3))  # per axis: inside, on the low face, on the high face
+    tgt = np.where(snap == 1, lo, np.where(snap == 2, hi, tgt))
+    tgt[: n // 6] = np.array([400.0, 5.0, 50.0]) + rng.uniform(-2e-3, 2e-3, (n // 6, 3))
+    dirs = rng.normal(size=(n, 3))
+    small = np.array([0.0, -0.0, 1e-30, -5e-324, 1e-21, -2e-20, 1e-19])
+    for j in range(3):
+        pick = rng.random(n) < 0.4
+        dirs[pick, j] = rng.choice(small, pick.sum())
+    keep = np.abs(dirs).max(axis=1) > 1e-3
+    tgt, dirs = tgt[keep], dirs[keep]
+    org = tgt - dirs * rng.uniform(50.0, 900.0, (len(tgt), 1)) / np.linalg.norm(dirs, axis=1)[:, None]
+    rays = np.concatenate([org, dirs, np.full((len(org), 1), 0.001), np.full((len(org), 1), np.inf)], axis=1)
+    h, o = yart.DeviceScene(d).intersect(rays)
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2
+    _hits_equal(h, o, h2, o2)
+
+
 @pytest.mark.parametrize("scene", ["sycee", "david"])
 def test_mesh_cull_box_is_exact_on_grazing_rays(dev, scene):
     """A ray whose conservative f32 test misses a mesh's cull box (the union of both roots' child
@@ -310,6 +344,37 @@ def test_world_bvh_forced_on_matches_linear_scan(dev, scene, opt):
     cam = p.camera(W, H)
     np.testing.assert_array_equal(s.render(cam, yart.render_params(W, H, spp, 50)),
                                   O.OracleScene(p.desc).render(cam, yart.render_params(W, H, spp, 50)))
+
+
+@pytest.mark.parametrize("world_bvh", [0, 1])
+def test_rays_in_face_planes_match_oracle(dev, opt, world_bvh):
+    """A ray lying exactly in a rect's plane (d[a] == 0 and o[a] == its k) gets t = 0 / 0 = NaN in
+    the reference's rect test, and a NaN t passes the range and bounds tests: the reference reports
+    a hit (t = NaN) wherever the ray runs, outside the rect too. Neither the box entity's f32 cull
+    nor the world BVH's node culling may drop such an object (r05: both did, since r02 / r03; such
+    rays now skip the cull / take the list walk). The cornell box's walls, light and the boxes'
+    faces (the rotated boxes' bottom face lies in y = 0 in their frame too), list walk and forced
+    world BVH: closest hits bitwise the oracle's."""
+    opt("world_bvh", world_bvh)
+    p = yart.Preset("cornell-box")
+    s = yart.DeviceScene(p)
+    assert (s.info().world_nodes > 0) == (world_bvh == 1)
+    rng = np.random.default_rng(43)
+    n = 40000
+    org = rng.uniform(0.0, 555.0, (n, 3))
+    dirs = rng.normal(size=(n, 3))
+    ax = rng.integers(0, 3, n)
+    planes = {0: [0.0, 555.0, 213.0, 343.0], 1: [0.0, 555.0, 554.0, 165.0, 330.0], 2: [555.0, 227.0, 332.0]}
+    inplane = rng.random(n) < 0.7
+    for a in range(3):
+        rows = np.nonzero((ax == a) & inplane)[0]
+        org[rows, a] = rng.choice(planes[a], len(rows))
+    dirs[np.arange(n), ax] = rng.choice([0.0, -0.0], n)
+    rays = np.concatenate([org, dirs, np.full((n, 1), 0.001), np.full((n, 1), np.inf)], axis=1)
+    h, o = s.intersect(rays)
+    h2, o2 = O.OracleScene(p.desc).intersect(rays)
+    assert (o2 >= 0).mean() > 0.2 and np.isnan(h2[:, 0][o2 >= 0]).any()  # NaN-t "hits" are among them
+    _hits_equal(h, o, h2, o2)
 
 
 @pytest.mark.parametrize("n", [17, 64, 257, 600])

@@ -603,6 +603,10 @@ __device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, doubl
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
   if (!(fabsf(chk) <= 3.0e38f)) return true;  // NaN / inf / near-overflow: do not cull
+  // A ray lying exactly in a face's plane (d[a] == 0, o[a] == the face's k) gets t = 0 / 0 = NaN in
+  // rect_t, and a NaN t passes its range and bounds tests: the reference "hits" that face wherever
+  // the ray runs. Such rays (an exactly zero direction component) are never culled.
+  if (r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0) return true;
   const float bmn[3] = {fminf((float)p[0], (float)p[3]), fminf((float)p[1], (float)p[4]), fminf((float)p[2], (float)p[5])};
   const float bmx[3] = {fmaxf((float)p[0], (float)p[3]), fmaxf((float)p[1], (float)p[4]), fmaxf((float)p[2], (float)p[5])};
   const float B = fmaxf(fmaxf(fmaxf(fabsf(bmn[0]), fabsf(bmn[1])), fmaxf(fabsf(bmn[2]), fabsf(bmx[0]))),
@@ -1562,7 +1566,10 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
-  if (!(fabsf(chk) <= 3.0e38f)) return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
+  // Non-finite rays, and rays with an exactly zero direction component (which can lie in a rect's
+  // plane, where rect_t's NaN t "hits" it outside any box, see box_may_hit), take the list walk.
+  if (!(fabsf(chk) <= 3.0e38f) || r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0)
+    return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
   float inv[3];
   bool use[3];
 #pragma unroll
