@@ -460,7 +460,8 @@ enum {
                                   stacks overflowing into HBM) | 1: the wavefront path for every mesh scene
                                   without media / moving spheres / noise or image textures */
   YART_OPT_WF_POOL = 6,        /* wavefront path slots, >= 256 (rounded down to a multiple of 256), default 2^20 */
-  YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass in bytes, default 4 GiB        */
+  YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass and stream in bytes; 0 (default) =
+                                  auto: min(64 GiB, a quarter of the device's memory)               */
   YART_OPT_COUNT = 8
 };
 int yart_debug_set_option(int option, int64_t value);

@@ -2,7 +2,7 @@
 
 The GPU renders each config's FULL frame exactly as bench.py / tools/bench_configs.py do (one
 yart_render call, samples_per_unit = 0: the library's own chunk/pass plan, so C2 runs the
-8-10-spp units of its persistent-wave plan and C5 the multi-pass scratch path). The oracle
+8-10-spp units of its persistent-wave plan; C5 in one scratch pass, and in 12 under a 4 GiB budget). The oracle
 (oracle/, the CPU restatement of main.rs:628-708) then renders either the same full frame (C1, C2:
 cheap enough) or only a fixed, spread subset of 8x8 blocks (b % stride == 0, through the same
 shard rule), and the two must be BITWISE equal on every pixel the oracle rendered.
@@ -59,10 +59,20 @@ def test_config_full_frame_bitwise(cfg, scene, W, H, spp, depth, stride):
     assert (gpu[cov].sum(axis=-1) != 0).mean() > 0.5
 
 
-def test_c5_runs_the_multi_pass_scratch_path():
-    """C5 on one device does not fit the 4 GiB per-sample scratch in one pass (49.8 MB per sample);
-    the plan must split it, which is what test_config_full_frame_bitwise[C5] then exercises."""
-    W, H, spp = 1920, 1080, 1024
+def test_c5_in_one_pass_and_in_scratch_passes_agree():
+    """C5's sample scratch is 49.8 MB per sample, 51 GB for the frame: the auto budget (min(64 GiB,
+    device memory / 4), capi.cpp scratch_budget) renders it in ONE pass on an MI355X, the old
+    4 GiB budget in 12 passes, each with its own accumulate. The two plans must give the same
+    frame bit for bit (k_accumulate adds samples in sample order whatever the split), so the
+    oracle check of test_config_full_frame_bitwise[C5] covers both."""
+    W, H, spp, depth = 1920, 1080, 1024, 50
     per_sample = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 3 * 8
-    assert per_sample * spp > 4 << 30
-    assert (4 << 30) // per_sample < spp
+    assert yart.get_option("scratch_bytes") == 0  # auto
+    assert per_sample * spp <= 64 << 30 and (4 << 30) // per_sample < spp
+    p = yart.Preset("david")
+    cam = p.camera(W, H)
+    s = yart.DeviceScene(p)
+    one = s.render(cam, yart.render_params(W, H, spp, depth))
+    with yart.option("scratch_bytes", 4 << 30):
+        split = s.render(cam, yart.render_params(W, H, spp, depth))
+    assert np.array_equal(one, split)

@@ -13,6 +13,7 @@
 #   rehearse bench.py's per-rank N = 2 path on one GPU (both ranks on device 0, gloo gather)
 #   configs  tools/bench_configs.py over every BASELINE config; with PMC summaries of the C4 / C5
 #            frames present in profiles/ (tools/summarize_profiles.py), the counter HBM bytes too
+#   configs_full  every BASELINE config at its full spp (no work counters)
 # Raw outputs under gpurun_out/; tools/summarize_profiles.py turns them into profiles/ files.
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$REPO/gpurun_out; mkdir -p "$OUT"; cd "$REPO"
@@ -43,6 +44,7 @@ for s in $STEPS; do
       [ -f profiles/${TAG}_c4_pmc.json ] && PM="$PM --pmc C4=profiles/${TAG}_c4_pmc.json"
       [ -f profiles/${TAG}_c5_pmc.json ] && PM="$PM --pmc C5=profiles/${TAG}_c5_pmc.json"
       run ${TAG}_bench_configs 900 python3 tools/bench_configs.py --spp-scale 0.0625 $PM ;;
+    configs_full) run ${TAG}_bench_configs_full 600 python3 tools/bench_configs.py --spp-scale 1.0 --no-stats --configs C1,C2,C3,C4,C5-shard,C5 ;;
   esac
 done
 echo ALL_OK

@@ -41,7 +41,7 @@ static std::atomic<int64_t> g_opt[YART_OPT_COUNT] = {
     {-1},       // YART_OPT_WORLD_BVH
     {-1},       // YART_OPT_MESH_WAVEFRONT
     {1 << 20},  // YART_OPT_WF_POOL
-    {4ll << 30} // YART_OPT_SCRATCH_BYTES
+    {0}         // YART_OPT_SCRATCH_BYTES (0 = auto: min(64 GiB, device memory / 4))
 };
 int64_t opt(int k) { return k >= 0 && k < YART_OPT_COUNT ? g_opt[k].load(std::memory_order_relaxed) : 0; }
 int hip_fail(hipError_t e, const char* what) {
@@ -278,6 +278,10 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
   DeviceGuard guard(device);
   if (hipDeviceGetAttribute(&s->cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || s->cu_count <= 0)
     s->cu_count = 256;
+  {
+    size_t total = 0;
+    if (hipDeviceTotalMem(&total, device) == hipSuccess) s->mem_total = total;
+  }
   uint64_t bytes = 0;
   DevScene& ds = s->dev;
   const auto up0 = std::chrono::steady_clock::now();
@@ -533,6 +537,18 @@ namespace {
 // frames) the samples are split into chunks; each sample's value then goes to HBM and
 // k_accumulate adds them per pixel in sample order, so the sums do not depend on the split.
 struct Plan { uint32_t chunk, pass_spp; };
+
+// Sample-scratch bytes one pass may use on a stream. Auto (option 0): a quarter of the device's
+// memory, at most 64 GiB — C5 (david 1920x1080x1024, 49.8 MB per sample) then runs in one pass on
+// an MI355X instead of 12 passes at the old 4 GiB, each of which drained the persistent waves
+// (279.7 -> 319.9 Msamples/s at full spp, profiles/r05j_c5_scratch_sweep.log). Two streams in
+// flight hold at most half the device.
+uint64_t scratch_budget(const yart_scene* s) {
+  const int64_t v = opt(YART_OPT_SCRATCH_BYTES);
+  if (v > 0) return (uint64_t)v;
+  const uint64_t cap = 64ull << 30;
+  return s->mem_total ? std::min<uint64_t>(cap, s->mem_total / 4) : (4ull << 30);
+}
 Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
   const uint32_t spp = a.spp;
   if (spp == 0 || a.n_blocks == 0) return {spp ? spp : 1, spp};
@@ -550,7 +566,7 @@ Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
     chunk = (uint32_t)((spp + chunks - 1) / chunks);
   }
   const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
-  const uint64_t budget = (uint64_t)std::max<int64_t>(opt(YART_OPT_SCRATCH_BYTES), 1);
+  const uint64_t budget = scratch_budget(s);
   uint64_t pass = budget / per_sample;
   pass = pass / chunk * chunk;
   if (pass < chunk) pass = chunk;
@@ -582,7 +598,6 @@ int stream_scratch(StreamState* st, hipStream_t stream, size_t bytes, double** o
   return YART_OK;
 }
 
-// n timing events for one frame (copied out: the caller owns them until push_frame hands them over).
 // The walk stacks' HBM overflow of a stream (deep meshes), grown on demand like the scratch.
 int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out) {
   if (st->ovf_bytes < bytes) {
@@ -598,6 +613,7 @@ int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out
   return YART_OK;
 }
 
+// n timing events for one frame (copied out: the caller owns them until push_frame hands them over).
 int take_events(yart_scene* s, size_t n, std::vector<hipEvent_t>& f) {
   f.clear();
   std::lock_guard<std::mutex> lk(s->mu);

@@ -68,6 +68,7 @@ struct Progress {
 struct yart_scene {
   int device = 0;
   int cu_count = 256;
+  uint64_t mem_total = 0;  // device memory (hipDeviceTotalMem): sizes the auto scratch budget
   bool wavefront = false;  // mesh scene without EXT features: k_wf_shade / k_wf_trace (deep meshes, YART_OPT_MESH_WAVEFRONT)
   uint32_t wf_pool = 1u << 20;  // paths in flight (YART_OPT_WF_POOL)
   yart_dev::DevScene dev{};
