@@ -44,7 +44,7 @@ for s in $STEPS; do
       [ -f profiles/${TAG}_c4_pmc.json ] && PM="$PM --pmc C4=profiles/${TAG}_c4_pmc.json"
       [ -f profiles/${TAG}_c5_pmc.json ] && PM="$PM --pmc C5=profiles/${TAG}_c5_pmc.json"
       run ${TAG}_bench_configs 900 python3 tools/bench_configs.py --spp-scale 0.0625 $PM ;;
-    configs_full) run ${TAG}_bench_configs_full 600 python3 tools/bench_configs.py --spp-scale 1.0 --no-stats --configs C1,C2,C3,C4,C5-shard,C5 ;;
+    configs_full) run ${TAG}_bench_configs_full 600 python3 tools/bench_configs.py --spp-scale 1.0 --no-stats ;;
   esac
 done
 echo ALL_OK
