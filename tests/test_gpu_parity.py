@@ -691,6 +691,32 @@ def test_chunked_multi_pass_and_shards(dev, opt):
     np.testing.assert_array_equal(parts[0] + parts[1], ref)
 
 
+def test_scratch_pass_shrinks_when_the_device_is_nearly_full(dev):
+    """The auto scratch budget (min(64 GiB, device memory / 4), capi.cpp scratch_budget) is sized
+    from the device's total memory, not what is free. With all but ~1.5 GB of the device held by
+    another allocation, a 1920x1080x64 frame (3.2 GB of sample scratch in one pass) cannot get
+    its pass: pass_scratch halves it until the allocation fits (64 -> 32 -> 16 samples), and the
+    frame is bitwise the one rendered 8 samples per pass with the device free."""
+    import torch
+    p = yart.Preset("cornell-box")
+    W, H, spp = 1920, 1080, 64
+    cam = p.camera(W, H)
+    prm = yart.render_params(W, H, spp, 50)
+    with yart.option("scratch_bytes", 8 * ((W + 7) // 8) * ((H + 7) // 8) * 64 * 24):
+        ref = yart.DeviceScene(p).render(cam, prm)
+    s = yart.DeviceScene(p)
+    free, _ = torch.cuda.mem_get_info(0)
+    hold = torch.empty(max(0, free - (3 << 29)), dtype=torch.uint8, device="cuda:0")
+    try:
+        assert torch.cuda.mem_get_info(0)[0] < 3 << 30  # the one-pass scratch cannot fit
+        got = s.render(cam, prm)
+    finally:
+        del hold
+        torch.cuda.empty_cache()
+    np.testing.assert_array_equal(got, ref)
+    assert (got[O.coverage(W, H)].sum(axis=-1) != 0).mean() > 0.5
+
+
 def test_auto_chunking_at_full_device_scale(dev):
     """A small frame on a 256-CU device is auto-split into sample chunks; still bitwise."""
     p = yart.Preset("cornell-box")

@@ -581,23 +581,6 @@ StreamState* stream_state(yart_scene* s, hipStream_t stream) {
   return e.get();
 }
 
-// Scratch of a stream, grown on demand. Called with st->frame_mu held: no other frame of this
-// library is being enqueued on the stream; earlier frames may still run on it, so the old buffer
-// is released only after the stream drained.
-int stream_scratch(StreamState* st, hipStream_t stream, size_t bytes, double** out) {
-  if (st->bytes < bytes) {
-    if (st->scratch) {
-      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its scratch");
-      HIP_TRY(hipFree(st->scratch), "hipFree scratch");
-    }
-    st->scratch = nullptr; st->bytes = 0;
-    HIP_TRY(hipMalloc(&st->scratch, bytes), "hipMalloc scratch");
-    st->bytes = bytes;
-  }
-  *out = st->scratch;
-  return YART_OK;
-}
-
 // The walk stacks' HBM overflow of a stream (deep meshes), grown on demand like the scratch.
 int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out) {
   if (st->ovf_bytes < bytes) {
@@ -611,6 +594,33 @@ int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out
   }
   *out = st->ovf;
   return YART_OK;
+}
+
+// Scratch of a stream for one pass of pl.pass_spp samples (+ 256 B for the unit counter), grown on
+// demand. Called with st->frame_mu held: no other frame of this library is being enqueued on the
+// stream; earlier frames may still run on it, so the old buffer is released only after the stream
+// drained. When the device cannot hold that much (the auto budget is sized from its total memory,
+// not from what is free: other scenes, streams or the caller's own allocations may hold the rest),
+// the pass shrinks by halves, down to one unit (`min_spp` samples), instead of failing the frame:
+// more passes, the same frame (k_accumulate adds in sample order whatever the split).
+int pass_scratch(StreamState* st, hipStream_t stream, const RenderArgs& a, Plan& pl, uint32_t min_spp,
+                 double** out) {
+  for (;;) {
+    const size_t bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double) + 256;
+    if (st->bytes >= bytes) { *out = st->scratch; return YART_OK; }
+    if (st->scratch) {
+      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its scratch");
+      HIP_TRY(hipFree(st->scratch), "hipFree scratch");
+    }
+    st->scratch = nullptr; st->bytes = 0;
+    const hipError_t e = hipMalloc(&st->scratch, bytes);
+    if (e == hipSuccess) { st->bytes = bytes; *out = st->scratch; return YART_OK; }
+    st->scratch = nullptr;
+    if (e != hipErrorOutOfMemory || pl.pass_spp <= min_spp) return hip_fail(e, "hipMalloc scratch");
+    (void)hipGetLastError();  // clear the allocation failure and try half the pass
+    uint32_t half = pl.pass_spp / 2 / min_spp * min_spp;
+    pl.pass_spp = half < min_spp ? min_spp : half;
+  }
 }
 
 // n timing events for one frame (copied out: the caller owns them until push_frame hands them over).
@@ -754,15 +764,14 @@ int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t str
 namespace yart_impl {
 
 int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream, Progress* prog) {
-  const Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
+  Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
   StreamState* st = stream_state(s, stream);
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
   if (prog) { a.progress = prog->device; a.progress_count = prog->counter; }
   if (s->wavefront && !stats) {  // mesh scenes: the wavefront path, pass by pass over the scratch budget
     double* scratch = nullptr;
-    const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
-    if (int rc = stream_scratch(st, stream, scratch_bytes + 256, &scratch)) return rc;
+    if (int rc = pass_scratch(st, stream, a, pl, 1, &scratch)) return rc;
     const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
     if (int rc = take_events(s, 3 * (size_t)passes, ev)) return rc;
     uint32_t k = 0;
@@ -800,8 +809,8 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     return YART_OK;
   }
   double* scratch = nullptr;
+  if (int rc = pass_scratch(st, stream, a, pl, pl.chunk, &scratch)) return rc;
   const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
-  if (int rc = stream_scratch(st, stream, scratch_bytes + 256, &scratch)) return rc;  // + the unit counter
   uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + scratch_bytes);
   const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
   if (int rc = take_events(s, 3 * (size_t)passes, ev)) return rc;
