@@ -462,7 +462,9 @@ enum {
   YART_OPT_WF_POOL = 6,        /* wavefront path slots, >= 256 (rounded down to a multiple of 256), default 2^20 */
   YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass and stream in bytes; 0 (default) =
                                   auto: min(64 GiB, a quarter of the device's memory)               */
-  YART_OPT_COUNT = 8
+  YART_OPT_UNITS_PER_WAVE = 8, /* persistent-wave plan: work units per resident wave; 0 (default) = auto:
+                                  64 for list-walk scenes, 192 with a mesh or the world BVH          */
+  YART_OPT_COUNT = 9
 };
 int yart_debug_set_option(int option, int64_t value);
 int yart_debug_get_option(int option, int64_t* value);

@@ -41,7 +41,8 @@ static std::atomic<int64_t> g_opt[YART_OPT_COUNT] = {
     {-1},       // YART_OPT_WORLD_BVH
     {-1},       // YART_OPT_MESH_WAVEFRONT
     {1 << 20},  // YART_OPT_WF_POOL
-    {0}         // YART_OPT_SCRATCH_BYTES (0 = auto: min(64 GiB, device memory / 4))
+    {0},        // YART_OPT_SCRATCH_BYTES (0 = auto: min(64 GiB, device memory / 4))
+    {0}         // YART_OPT_UNITS_PER_WAVE (0 = auto: 64 list walk, 192 mesh / world BVH)
 };
 int64_t opt(int k) { return k >= 0 && k < YART_OPT_COUNT ? g_opt[k].load(std::memory_order_relaxed) : 0; }
 int hip_fail(hipError_t e, const char* what) {
@@ -557,12 +558,21 @@ Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
     if (requested >= spp) return {spp, spp};  // explicit one-unit-per-block: the fused kernel
     chunk = requested;
   } else {
-    // Persistent waves (4 per SIMD x 4 SIMDs per CU) pull units from a queue; ~64 units per
-    // wave keeps the end-of-frame imbalance small (cornell 800x800x256: 64 units/wave = 8-10
-    // samples per unit, 4,130 Msamples/s, against 3,996 at 32 and 2,615 at 256).
-    const uint64_t target = 64ull * (uint64_t)s->cu_count * 16ull;
+    // Persistent waves (4 per SIMD x 4 SIMDs per CU) pull units from a queue; many units per
+    // wave keep the end-of-frame imbalance small, each unit's start costs a little. The list walk
+    // (cornell: cheap samples) is best at ~64 units per wave (r02: 4,130 Msamples/s against 3,996
+    // at 32 and 2,615 at 256; r05l: 64 within 0.5 % of 32-128); mesh and world-BVH frames, whose
+    // samples cost 1.5-20x more and vary more, at ~192 (r05l at BASELINE spp: C4 +4.4 %, C5 shard
+    // +1.1 %, C5 +0.8 %, C3 +0.4 % over 64), but not below 2 samples per unit (C3 1200x800x31:
+    // -2.8 %, C4 800x800x32: -1.9 % at one sample; profiles/r05l_units_per_wave_sweep.log).
+    const bool heavy = s->dev.has_mesh || s->dev.world_nodes;
+    int64_t upw = opt(YART_OPT_UNITS_PER_WAVE);
+    if (upw <= 0) upw = heavy ? 192 : 64;
+    const uint64_t target = (uint64_t)upw * (uint64_t)s->cu_count * 16ull;
     uint64_t chunks = (target + a.n_blocks - 1) / a.n_blocks;
-    if (chunks > spp) chunks = spp;
+    const uint32_t min_chunk = heavy && spp >= 2 ? 2 : 1;
+    const uint64_t max_chunks = (spp + min_chunk - 1) / min_chunk;  // 31 spp: 16 units of <= 2
+    if (chunks > max_chunks) chunks = max_chunks;
     chunk = (uint32_t)((spp + chunks - 1) / chunks);
   }
   const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
