@@ -696,8 +696,12 @@ def test_scratch_pass_shrinks_when_the_device_is_nearly_full(dev):
     from the device's total memory, not what is free. With all but ~1.5 GB of the device held by
     another allocation, a 1920x1080x64 frame (3.2 GB of sample scratch in one pass) cannot get
     its pass: pass_scratch halves it until the allocation fits (64 -> 32 -> 16 samples), and the
-    frame is bitwise the one rendered 8 samples per pass with the device free."""
-    import torch
+    frame is bitwise the one rendered 8 samples per pass with the device free. The hold goes
+    through the HIP runtime libyart links (the same instance, already loaded), not torch's."""
+    hip = C.CDLL("/opt/rocm/lib/libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemGetInfo.argtypes = [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
     p = yart.Preset("cornell-box")
     W, H, spp = 1920, 1080, 64
     cam = p.camera(W, H)
@@ -705,14 +709,16 @@ def test_scratch_pass_shrinks_when_the_device_is_nearly_full(dev):
     with yart.option("scratch_bytes", 8 * ((W + 7) // 8) * ((H + 7) // 8) * 64 * 24):
         ref = yart.DeviceScene(p).render(cam, prm)
     s = yart.DeviceScene(p)
-    free, _ = torch.cuda.mem_get_info(0)
-    hold = torch.empty(max(0, free - (3 << 29)), dtype=torch.uint8, device="cuda:0")
+    free, total = C.c_size_t(), C.c_size_t()
+    assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+    hold = C.c_void_p()
+    assert hip.hipMalloc(C.byref(hold), max(1, free.value - (3 << 29))) == 0
     try:
-        assert torch.cuda.mem_get_info(0)[0] < 3 << 30  # the one-pass scratch cannot fit
+        assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+        assert free.value < 3 << 30  # the one-pass scratch cannot fit
         got = s.render(cam, prm)
     finally:
-        del hold
-        torch.cuda.empty_cache()
+        assert hip.hipFree(hold) == 0
     np.testing.assert_array_equal(got, ref)
     assert (got[O.coverage(W, H)].sum(axis=-1) != 0).mean() > 0.5
 

@@ -18,8 +18,8 @@ rep('''  uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH
 '''  uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   double* const cq = &s_cam[CQ ? wave * 2 * 7 * 64 + lane : 0];
   uint32_t cq_have0 = 0xFFFFFFFFu, cq_have1 = 0xFFFFFFFFu;  // the group each buffer holds (wave-uniform)''')
-rep('''          local_blk = u % A.n_blocks; chunk_id = u / A.n_blocks;''',
-'''          local_blk = u % A.n_blocks; chunk_id = u / A.n_blocks;
+rep('''          local_blk = u / A.n_chunks; chunk_id = u % A.n_chunks;''',
+'''          local_blk = u / A.n_chunks; chunk_id = u % A.n_chunks;
           cq_have0 = 0xFFFFFFFFu; cq_have1 = 0xFFFFFFFFu;''')
 rep('''        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const uint32_t avail = n_jobs - next_job;''',

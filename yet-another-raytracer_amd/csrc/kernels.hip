@@ -2217,7 +2217,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
           }
           const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)first);
           if (u >= A.n_units) { drained = true; break; }
-          local_blk = u % A.n_blocks; chunk_id = u / A.n_blocks;
+          // block-major: a block's sample chunks are consecutive units, so the waves in flight
+          // work on a compact patch of the frame (coherent camera rays and first hits, the same
+          // mesh nodes in L2): bitwise the same, +0.6 % cornell, +1.5 % david, +1.9 % random-scene,
+          // +4.2 % bunny over chunk-major (profiles/r05m_ab_unit_order.log)
+          local_blk = u / A.n_chunks; chunk_id = u % A.n_chunks;
           b = A.shard_index + local_blk * A.shard_count;
           bx0 = (b % A.blocks_x) * 8; by0 = (b / A.blocks_x) * 8;
           s_lo = A.s_begin + chunk_id * A.chunk;
