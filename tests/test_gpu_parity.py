@@ -697,8 +697,9 @@ def test_scratch_pass_shrinks_when_the_device_is_nearly_full(dev):
     another allocation, a 1920x1080x64 frame (3.2 GB of sample scratch in one pass) cannot get
     its pass: pass_scratch halves it until the allocation fits (64 -> 32 -> 16 samples), and the
     frame is bitwise the one rendered 8 samples per pass with the device free. The hold goes
-    through the HIP runtime libyart links (the same instance, already loaded), not torch's."""
-    hip = C.CDLL("/opt/rocm/lib/libamdhip64.so.7")
+    through the HIP runtime libyart uses: opened by soname, dlopen returns the copy already
+    loaded (torch's, when torch was imported first; /opt/rocm's otherwise)."""
+    hip = C.CDLL("libamdhip64.so.7")
     hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
     hip.hipFree.argtypes = [C.c_void_p]
     hip.hipMemGetInfo.argtypes = [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
