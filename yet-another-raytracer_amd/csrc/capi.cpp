@@ -837,8 +837,7 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     b.waves = (uint32_t)s->cu_count * 16;  // 4 waves per SIMD resident
     b.progress_base = base;
     base += b.n_units;
-    // the unit counter, and the 8 XCD-local ones of mesh frames (kernels.hip, claim of a unit)
-    HIP_TRY(hipMemsetAsync(queue, 0, 9 * sizeof(uint32_t), stream), "zero the unit counters");
+    HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream), "zero the unit counter");
     HIP_TRY(hipEventRecord(ev[3 * k], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
     HIP_TRY(hipEventRecord(ev[3 * k + 1], stream), "hipEventRecord");

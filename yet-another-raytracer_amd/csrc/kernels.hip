@@ -2210,34 +2210,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
           const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
           uint32_t v = 0;
           if (lane == first) {
-            if (HAS_MESH) {
-              // XCD-local queues (mesh frames): workgroups are dealt to the 8 XCDs round-robin, so
-              // XCD x takes the units of its own eighth of the frame first (its L2 then holds that
-              // patch's mesh nodes), then steals from the others in turn; a partition is empty once
-              // its counter passes its size, and every claim ends with a unit or after 8 tries.
-              // Same-box A/B: david +1.5 %, bunny +1.9 %; the list walk (cornell -1.2 %) and the
-              // world BVH (random-scene -0.2 %) keep the one counter (profiles/r05n_ab_xcd_queues.log).
-              v = 0xFFFFFFFFu;
-              const uint32_t x0 = blockIdx.x & 7u;
-              for (uint32_t k = 0; k < 8u; ++k) {
-                const uint32_t x = (x0 + k) & 7u;
-                const uint32_t lo = (uint32_t)(((uint64_t)A.n_units * x) >> 3);
-                const uint32_t hi = (uint32_t)(((uint64_t)A.n_units * (x + 1u)) >> 3);
-                if (hi <= lo) continue;
-                const uint32_t t = atomicAdd(A.queue + 1 + x, 1u);
-                if (t < hi - lo) { v = lo + t; break; }
-              }
-              if (A.progress) {  // the units handed out so far, counted on queue[0]
-                const uint32_t c = v < A.n_units ? atomicAdd(A.queue, 1u) + 1u : A.n_units;
-                __hip_atomic_store(A.progress, A.progress_base + (c < A.n_units ? c : A.n_units), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-              }
-            } else {
-              v = atomicAdd(A.queue, 1u);
-              if (A.progress)  // yart_render's progress: the units handed out so far (host-mapped word)
-                __hip_atomic_store(A.progress, A.progress_base + (v < A.n_units ? v + 1u : A.n_units), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            v = atomicAdd(A.queue, 1u);
+            if (A.progress)  // yart_render's progress: the units handed out so far (host-mapped word)
+              __hip_atomic_store(A.progress, A.progress_base + (v < A.n_units ? v + 1u : A.n_units), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
           }
           const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)first);
           if (u >= A.n_units) { drained = true; break; }
