@@ -25,7 +25,7 @@ cli: $(BIN)/yart
 oracle:
 	$(MAKE) -C $(ROOT)/oracle
 
-$(GEN)/cie_xyz.inc $(GEN)/smits.inc: $(ROOT)/tables/cie1931_xyz_1nm_360_830.f64 $(ROOT)/tables/smits_basis_36bin.f64 $(ROOT)/tools/gen_tables_inc.py
+$(GEN)/cie_xyz.inc $(GEN)/smits.inc $(GEN)/srgb_steps.inc: $(ROOT)/tables/cie1931_xyz_1nm_360_830.f64 $(ROOT)/tables/smits_basis_36bin.f64 $(ROOT)/tables/srgb_u8_steps.f64 $(ROOT)/tools/gen_tables_inc.py
 	python3 $(ROOT)/tools/gen_tables_inc.py $(GEN)
 
 $(LIB)/libyart_host.so: $(HOST_SRCS) $(HOST_HDRS)
@@ -34,7 +34,7 @@ $(LIB)/libyart_host.so: $(HOST_SRCS) $(HOST_HDRS)
 
 # build/gen/build_id.h: sha256 of the sources (yart/buildid.py), returned by yart_build_id(); the
 # Python side refuses a libyart.so whose id is not the tree's (a stale prebuilt library)
-$(LIB)/libyart.so: $(DEV_SRCS) $(DEV_HDRS) $(GEN)/cie_xyz.inc $(GEN)/smits.inc $(ROOT)/Makefile
+$(LIB)/libyart.so: $(DEV_SRCS) $(DEV_HDRS) $(GEN)/cie_xyz.inc $(GEN)/smits.inc $(GEN)/srgb_steps.inc $(ROOT)/Makefile
 	@mkdir -p $(LIB)
 	python3 $(PKG)/yart/buildid.py --header $(GEN)/build_id.h
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(DEV_SRCS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
@@ -49,7 +49,7 @@ clean:
 .PHONY: all host device cli oracle clean
 
 # A/B builds for tools/ab.py: make variant NAME=x DEFS="-DYART_FOO"
-variant: $(GEN)/cie_xyz.inc $(GEN)/smits.inc
+variant: $(GEN)/cie_xyz.inc $(GEN)/smits.inc $(GEN)/srgb_steps.inc
 	@mkdir -p $(LIB)/variants
 	python3 $(PKG)/yart/buildid.py --header $(GEN)/build_id.h
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o $(LIB)/variants/libyart_$(NAME).so $(DEV_SRCS) -L/opt/rocm/lib -lrccl

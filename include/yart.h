@@ -436,8 +436,10 @@ int yart_world_bvh_build(const yart_scene_desc* desc, yart_world_bvh_info* out);
 /* The per-sample random stream: n draws of gen::<f64>() for (pixel, sample). */
 int yart_probe_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n,
                    double* out);
-/* Elementwise device math on n inputs: op 0 sqrt(a), 1 a/b, 2 sin(a), 3 cos(a), 4 pow(a,b),
- * 5 ln(a), 6 acos(a), 7 atan2(a,b) (3, 5-7: the deterministic fdlibm forms the kernels use). */
+/* Elementwise device math on n inputs: op 0 sqrt(a), 1 a/b, 2 sin(a), 3 cos(a), 4 pow(a,b)
+ * (the vendor's; no kernel uses it), 5 ln(a), 6 acos(a), 7 atan2(a,b) (2-3, 5-7: the deterministic
+ * fdlibm forms the kernels use), 8-10 the guarded fast sqrt / unit / quotient, 11 the 8-bit
+ * channel k_finalize gives the linear value a (gamma_corrected + clamp_display_channel). */
 int yart_probe_math(int device, int op, const double* a, const double* b, uint32_t n,
                     double* out);
 /* on != 0: every mesh ray whose front-to-back walk found a hit is walked again in the reference's

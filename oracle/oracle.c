@@ -519,6 +519,11 @@ static double gamma_channel(double linear) { /* color.rs:93-101 */
 void oracle_gamma_corrected(const double in[3], double out[3]) { /* color.rs:92-107 */
   out[0] = gamma_channel(in[0]); out[1] = gamma_channel(in[1]); out[2] = gamma_channel(in[2]);
 }
+/* The 8-bit channel of each linear value: gamma_channel (glibc's pow, as f64::powf) then
+ * clamp_display_channel, as main.rs:710-718 applies them; for tests/test_finalize_bytes.py. */
+void oracle_display_bytes(const double* linear, size_t n, uint8_t* out) {
+  for (size_t i = 0; i < n; ++i) out[i] = oracle_clamp_display_channel(gamma_channel(linear[i]));
+}
 uint8_t oracle_clamp_display_channel(double c) { /* main.rs:461-463; `as u8` saturates, NaN->0 */
   double v = c;
   if (v != v) v = 0.0; /* f64::clamp propagates NaN; 256*NaN as u8 = 0 */

@@ -20,6 +20,7 @@
 #ifndef YART_ORACLE_H
 #define YART_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 #include "../include/yart.h"
 
@@ -63,6 +64,7 @@ int oracle_obj_load(const char* path, float* positions, double* normals, double*
 void oracle_sanitize_sample_xyz(const double in[3], double out[3]);       /* main.rs:448-459 */
 uint8_t oracle_clamp_display_channel(double c);                          /* main.rs:461-463 */
 void oracle_gamma_corrected(const double in[3], double out[3]);          /* color.rs:92-107 */
+void oracle_display_bytes(const double* linear, size_t n, uint8_t* out);  /* gamma + clamp, bulk */
 void oracle_xyz_into_rgb(const double in[3], double out[3]);             /* color.rs:174-214 */
 void oracle_xyz_from_wavelength(double wl, double out[3]);               /* color.rs:216-228 */
 double oracle_rgb_reflect(const double rgb[3], double wl);               /* color.rs:54-90,160-164,276-283 */

@@ -47,6 +47,7 @@ def lib():
         "oracle_texture_probe": (D, [P, U32, D, P, D, D]),
         "oracle_acos": (D, [D]),
         "oracle_atan2": (D, [D, D]),
+        "oracle_display_bytes": (None, [P, C.c_size_t, P]),
         "oracle_obj_count": (I, [C.c_char_p, C.POINTER(U32)]),
         "oracle_obj_load": (I, [C.c_char_p, P, P, P, U32]),
     }
@@ -119,6 +120,15 @@ def finalize(xyz_sum, spp):
     x = np.ascontiguousarray(xyz_sum, dtype=np.float64)
     out = np.zeros((h, w, 4), dtype=np.uint8)
     assert lib().oracle_finalize_rgba8(_p(x), w, h, spp, _p(out)) == 0
+    return out
+
+
+def display_bytes(linear):
+    """The reference's 8-bit channel of each linear value (gamma_channel with glibc's pow, then
+    clamp_display_channel)."""
+    x = np.ascontiguousarray(linear, dtype=np.float64)
+    out = np.empty(x.shape, dtype=np.uint8)
+    lib().oracle_display_bytes(_p(x), x.size, _p(out))
     return out
 
 

@@ -57,6 +57,14 @@ def test_config_full_frame_bitwise(cfg, scene, W, H, spp, depth, stride):
     # the oracle rendered nothing outside its blocks; the GPU rendered everything covered
     assert (oracle[~m] == 0).all()
     assert (gpu[cov].sum(axis=-1) != 0).mean() > 0.5
+    # the product's output, the RGBA8 image (main.rs:710-718): the device's k_finalize of the GPU
+    # frame equals the oracle's finalize (glibc pow) of the oracle frame on every checked pixel, and
+    # the oracle's finalize of the GPU frame on every pixel of the frame
+    g8 = yart.finalize_rgba8(gpu, spp)
+    o8 = O.finalize(oracle, spp)
+    bad8 = np.argwhere((g8 != o8).any(axis=-1) & m)
+    assert len(bad8) == 0, f"{cfg}: {len(bad8)} RGBA8 pixels differ, e.g. (y, x) {bad8[:4].tolist()}"
+    np.testing.assert_array_equal(g8, O.finalize(gpu, spp))
 
 
 def test_c5_in_one_pass_and_in_scratch_passes_agree():

@@ -2,8 +2,8 @@
 
 Both sides evaluate the reference's hot path in IEEE f64 with the same counter-based RNG, so the
 bar is BITWISE equality, not a tolerance: every pixel sum, every hit record, every random draw.
-The only arithmetic the two do not share is libm's pow in finalize (ocml vs glibc), where the
-8-bit output is allowed to differ by 1 LSB on at most 0.1 % of channels.
+The one libm call the device cannot share, finalize's glibc pow, is replaced by the 255 steps of the
+reference's byte map (test_finalize_bytes.py), so the RGBA8 output is bitwise too.
 """
 import ctypes as C
 import math
@@ -920,10 +920,27 @@ def test_finalize_matches_oracle(dev):
     xyz = O.OracleScene(p.desc).render(p.camera(W, H), yart.render_params(W, H, spp, 50))
     g = yart.finalize_rgba8(xyz, spp)
     c = O.finalize(xyz, spp)
-    diff = np.abs(g.astype(int) - c.astype(int))
-    assert diff.max() <= 1
-    assert (diff > 0).mean() <= 1e-3
-    np.testing.assert_array_equal(g[..., 3], c[..., 3])
+    np.testing.assert_array_equal(g, c)
+    # bright, dark, negative and non-finite sums too (sanitize is upstream; finalize must still agree)
+    rng = np.random.default_rng(9)
+    wild = rng.normal(0.0, 1.0, (64, 96, 3)) * 10.0 ** rng.uniform(-6, 6, (64, 96, 1)) * spp
+    wild[0, :4] = [[np.nan, 0, 0], [np.inf, -np.inf, 0], [0, 0, 0], [-0.0, 1e308, -1e308]]
+    with np.errstate(all="ignore"):
+        np.testing.assert_array_equal(yart.finalize_rgba8(wild, spp), O.finalize(wild, spp))
+
+
+def test_device_byte_map_matches_reference_around_every_step(dev):
+    """k_finalize's srgb_byte (probe op 11) on every double within 512 ulps of each of the 255
+    steps and of the 0.0031308 branch edge, against the oracle's glibc-pow chain."""
+    from test_finalize_bytes import steps
+    centres = np.concatenate([steps(), [0.0031308]]).view(np.int64)
+    win = (centres[:, None] + np.arange(-512, 513, dtype=np.int64)[None, :]).ravel().view(np.float64)
+    rng = np.random.default_rng(10)
+    with np.errstate(all="ignore"):
+        win = np.concatenate([win, rng.uniform(-0.1, 1.2, 200000), 10.0 ** rng.uniform(-320, 308, 50000),
+                              [np.nan, np.inf, -np.inf, 0.0, -0.0]])
+        got = _probe(dev, 11, win)
+        np.testing.assert_array_equal(got, O.display_bytes(win).astype(np.float64))
 
 
 def test_errors_are_reported_not_raised(dev):

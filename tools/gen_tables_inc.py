@@ -2,7 +2,8 @@
 
 Used by the Makefile for both the HIP library and the oracle:
     python tools/gen_tables_inc.py <outdir>
-writes <outdir>/cie_xyz.inc (471 rows x (x,y,z)) and <outdir>/smits.inc (7 x 36).
+writes <outdir>/cie_xyz.inc (471 rows x (x,y,z)), <outdir>/smits.inc (7 x 36) and
+<outdir>/srgb_steps.inc (the 255 steps of the linear -> 8-bit map, tools/gen_srgb_steps.py).
 """
 import struct
 import sys
@@ -23,6 +24,7 @@ def main():
     out.mkdir(parents=True, exist_ok=True)
     emit("cie1931_xyz_1nm_360_830.f64", out / "cie_xyz.inc", 3)
     emit("smits_basis_36bin.f64", out / "smits.inc", 36)
+    emit("srgb_u8_steps.f64", out / "srgb_steps.inc", 255)
 
 
 if __name__ == "__main__":

@@ -2694,16 +2694,22 @@ __global__ __launch_bounds__(256, SLOTS == kCoopSlots ? kMeshWavesPerEu : 3) voi
 }
 
 // ------------------------------------------------------------------------ finalize
-__device__ __forceinline__ double gamma_channel(double linear) {  // color.rs:93-101
-  linear = fmax(linear, 0.0);
-  if (linear <= 0.0031308) return 12.92 * linear;
-  return 1.055 * pow(linear, 1.0 / 2.4) - 0.055;
-}
-__device__ __forceinline__ uint8_t display_channel(double c) {  // main.rs:461-463
-  if (c != c) return 0;
-  c = c < 0.0 ? 0.0 : (c > 0.999 ? 0.999 : c);
-  const double m = 256.0 * c;
-  return m >= 255.0 ? (uint8_t)255 : (uint8_t)(int)m;
+// gamma_corrected (color.rs:93-101) then clamp_display_channel (main.rs:461-463) is a monotone step
+// function of the linear channel, so it is its 255 steps: X_k = the least double whose byte is >= k,
+// derived with glibc's pow — the function the reference's f64::powf calls — by
+// tools/gen_srgb_steps.py. The byte is the count of steps at or below the value: the reference's
+// byte for every double (NaN and values <= 0 count none, +inf all 255), with no vendor pow, whose
+// last ulp differs from glibc's (tests/test_finalize_bytes.py checks every double within 4096 ulps
+// of every step). Branchless binary search: 8 compares.
+__constant__ double c_srgb_steps[255] =
+#include "srgb_steps.inc"
+    ;  // one brace-enclosed row of 255 hex floats
+__device__ __forceinline__ uint8_t srgb_byte(double linear) {
+  uint32_t n = 0;
+#pragma unroll
+  for (uint32_t s = 128; s != 0; s >>= 1)
+    if (linear >= c_srgb_steps[n + s - 1]) n += s;
+  return (uint8_t)n;
 }
 __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ xyz, uint32_t w, uint32_t h, uint32_t spp,
                                                   uint8_t* __restrict__ rgba) {  // main.rs:710-718
@@ -2717,8 +2723,7 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ xyz
     const double r = 2.6896552 * v.x - 1.2758621 * v.y - 0.4137931 * v.z;  // XYZ::into_rgb color.rs:209-213
     const double gg = -1.0221082 * v.x + 1.9782866 * v.y + 0.0438216 * v.z;
     const double b = 0.0612245 * v.x - 0.2244898 * v.y + 1.1632653 * v.z;
-    out = make_uchar4(display_channel(gamma_channel(r)), display_channel(gamma_channel(gg)),
-                      display_channel(gamma_channel(b)), 255);
+    out = make_uchar4(srgb_byte(r), srgb_byte(gg), srgb_byte(b), 255);
   }
   reinterpret_cast<uchar4*>(rgba)[i] = out;
 }
@@ -2765,6 +2770,7 @@ __global__ void k_probe_math(int op, const double* a, const double* b, uint32_t 
       }
       break;
     }
+    case 11: out[i] = (double)srgb_byte(a[i]); break;
     default: out[i] = pow(a[i], b[i]); break;
   }
 }
