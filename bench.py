@@ -30,6 +30,10 @@ Also reported on the same line:
   cpu_baseline  the CPU restatement (oracle/) on this host's cores, rank 0 only, on a bounded
                 sample of the same workload (same frame at fewer spp; Msamples/s is ~spp-invariant),
                 with the host's nproc, usable CPUs and CPU model.
+  david         BASELINE configs[4] (david 1920x1080, depth 50, the config BASELINE assigns to 8
+                GPUs) at --david-spp (default 64 = 1/16 of its 1024 spp), through the same N-GPU data
+                path: one warm-up and --david-frames timed frames after the headline's, ms per frame,
+                Msamples/s and the per-device render / gather times. A sub-record: `value` stays C2's.
 """
 import argparse
 import hashlib
@@ -86,6 +90,9 @@ def parse():
                          "the GPU box's share per GPU)")
     ap.add_argument("--no-stats", action="store_true", help="skip the instrumented launch (roofline = null)")
     ap.add_argument("--spu", type=int, default=0, help="samples per work unit (0 = library's choice)")
+    ap.add_argument("--david-spp", type=int, default=64,
+                    help="spp of the david (configs[4]) sub-record (0 = skip it)")
+    ap.add_argument("--david-frames", type=int, default=2, help="timed frames of the david sub-record")
     ap.add_argument("--streams", type=int, default=2,
                     help="frames alternate over this many HIP streams (2: the next frame's render fills the SIMD "
                          "slots the previous frame's last paths leave idle; 1: strictly one after another)")
@@ -178,6 +185,19 @@ def valu_issue(pmc):
         return None
 
 
+def valu_lanes(pmc):
+    """Active lanes per VALU instruction of the render kernel:
+    SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU, and the same ratio of k_accumulate from the same
+    pass (full 64-lane waves), which calibrates the two counters' units; `active_lanes` = 64 x the
+    kernel's ratio / k_accumulate's."""
+    r, c = pmc.get("valu_thread_per_active_inst"), pmc.get("calib_k_accumulate_thread_per_active_inst")
+    if r is None:
+        return None
+    return {"thread_cycles_per_active_inst": round(r, 3), "k_accumulate_ratio": round(c, 3) if c else None,
+            "active_lanes": round(64.0 * r / c, 2) if c else None,
+            "source": "SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU (PMC snapshot)"}
+
+
 def fp64_issue(pmc, kern_ms):
     """Hardware-counted FP64 work of the snapshot: SQ_INSTS_VALU_FLOPS_FP64 counts FLOPs per wave
     instruction (add/mul/trans 1, FMA 2); x 64 lanes, exec mask not applied, so an upper bound on
@@ -215,6 +235,124 @@ def launch_mode(a):
             sys.exit(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible; refusing to report another N")
         return "multi", a.gpus, 0, 0
     return "single", 1, 0, 0
+
+
+DAVID = dict(scene="david", width=1920, height=1080, max_depth=50)
+DAVID_FRAME_S = 0.5  # one GPU, 64 spp: ~0.41 s measured (r05m C5 324.5 Msamples/s), rounded up
+
+
+def david_record(a, mode, world, rank, local, dev, wd, comm, nccl_group, rehearse):
+    """The david sub-record (BASELINE configs[4] at --david-spp) over the launch's N-GPU path, after
+    the headline measurement: scene upload, one warm-up frame, a barrier, --david-frames frames
+    timed (max over ranks), per-device render / gather times, and for N > 1 the assembled frame
+    checked bitwise against a one-device render of the same frame."""
+    W, H, depth, spp = DAVID["width"], DAVID["height"], DAVID["max_depth"], a.david_spp
+    nfr = max(1, a.david_frames)
+    per_frame = DAVID_FRAME_S * spp / 64.0
+    deadline = lambda k: BASE_DEADLINE_S + 20.0 * per_frame * k  # noqa: E731
+    preset = yart.Preset(DAVID["scene"])
+    cam = preset.camera(W, H)
+    st = torch.cuda.current_stream(dev)
+    frame = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
+    scene = multi = None
+    with wd.stage(f"david: scene upload ({mode})", BASE_DEADLINE_S + 10.0 * world):
+        if mode == "multi":
+            multi = yart.MultiScene(preset, list(range(world)))
+        else:
+            scene = yart.DeviceScene(preset.desc, device=local)
+    if mode == "ranks":
+        prm = yart.render_params(W, H, spp, depth, shard_index=rank, shard_count=world)
+        packed = torch.zeros(yart.shard_packed_len(W, H, 0, world), dtype=torch.float64, device=dev)
+        pg = None if comm is not None else PackedGather(W, H, world, rank, torch.device("cpu") if rehearse else dev)
+    else:
+        prm = yart.render_params(W, H, spp, depth)
+    gtimes = []
+
+    def one():
+        if mode == "single":
+            scene.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
+        elif mode == "multi":
+            multi.render_async(cam, prm, frame.data_ptr(), st.cuda_stream)
+        else:
+            scene.render_packed_async(cam, prm, packed.data_ptr(), st.cuda_stream)
+            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g0.record(st)
+            if comm is not None:
+                comm.gather_frame_async(packed.data_ptr(), W, H, frame.data_ptr(), st.cuda_stream)
+            elif rehearse:
+                ph, fh = packed.cpu(), torch.zeros_like(frame, device="cpu")
+                pg(ph, fh, dist)
+                if rank == 0:
+                    frame.copy_(fh)
+            else:
+                pg(packed, frame, dist, group=nccl_group)
+            g1.record(st)
+            gtimes.append((g0, g1))
+
+    def timing():
+        if mode == "multi":
+            return multi.frame_timing()
+        return scene.frame_timing(st.cuda_stream)
+
+    with wd.stage("david: warm-up frame", deadline(1)):
+        one()
+        wait_events([_event(st)])
+    timing()
+    gtimes.clear()
+    if mode == "ranks":
+        with wd.stage("david: barrier before the timed frames", BASE_DEADLINE_S):
+            dist.barrier()
+    with wd.stage("david: timed frames", deadline(nfr)):
+        t0 = time.perf_counter()
+        for _ in range(nfr):
+            one()
+        wait_events([_event(st)])
+    if mode == "ranks":
+        with wd.stage("david: barrier after the timed frames", BASE_DEADLINE_S):
+            dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if mode == "ranks":
+        with wd.stage("david: max-over-ranks time", BASE_DEADLINE_S):
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+    render_ms, _, n = timing()
+    balance = None
+    if mode == "multi":
+        dr, dg, dn = multi.device_timing()
+        balance = device_balance([x / max(1, dn) for x in dr], [x / max(1, dn) for x in dg])
+    elif mode == "ranks":
+        mine = torch.tensor([render_ms / max(1, n), sum(x.elapsed_time(y) for x, y in gtimes) / max(1, len(gtimes))],
+                            dtype=torch.float64)
+        every = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+        with wd.stage("david: per-rank timings", BASE_DEADLINE_S):
+            dist.all_gather(every, mine)
+        balance = device_balance([float(t[0]) for t in every], [float(t[1]) for t in every])
+    else:
+        balance = device_balance([render_ms / max(1, n)], None)
+    check = None
+    if rank == 0 and world > 1:
+        with wd.stage("david: frame check (one-device render)", deadline(world)):
+            one_dev = scene if scene is not None else yart.DeviceScene(preset.desc, device=local)
+            full = torch.zeros_like(frame)
+            one_dev.render_async(cam, yart.render_params(W, H, spp, depth), full.data_ptr(), st.cuda_stream)
+            wait_events([_event(st)])
+        assert torch.equal(full, frame), "david: assembled frame differs from the one-device render"
+        check = "assembled frame bitwise equal to the one-device render"
+    if multi is not None:
+        multi.close()
+    samples = W * H * spp
+    return {"workload": f"david {W}x{H}x{spp}spp depth {depth} (BASELINE configs[4] at {spp}/1024 of its spp)",
+            "spp": spp, "warmup": 1, "frames": nfr, "n_gpus": world,
+            "ms_per_frame": round(elapsed / nfr * 1e3, 3),
+            "msamples_per_s": round(samples * nfr / elapsed / 1e6, 3),
+            "kernel_ms": round(render_ms / max(1, n), 3), "device_balance": balance, "frame_check": check}
+
+
+def _event(st):
+    ev = torch.cuda.Event()
+    ev.record(st)
+    return ev
 
 
 def main():
@@ -489,6 +627,7 @@ def main():
                     "record_byte_rate_of_hbm_peak": round((24 * (st.prim_tests + st.light_tests) + 128 * st.node_visits +
                                                            36 * st.leaf_tris) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "valu_issue_busy": valu_issue(pmc) if world == 1 else None,
+                    "valu_active_lanes": valu_lanes(pmc) if world == 1 else None,
                     "fp64_issued": fp64_issue(pmc, kern_ms) if world == 1 else None,
                     # wave-level VALU instructions (SQ_INSTS_VALU of the snapshot) per path segment
                     "valu_insts_per_segment": (round(pmc["SQ_INSTS_VALU"] / st.segments, 2)
@@ -497,6 +636,9 @@ def main():
             roofline["gather_ms"] = round(gather_ms, 3)
         if balance is not None:
             roofline.update(balance)
+    david = None
+    if a.david_spp > 0:
+        david = david_record(a, mode, world, rank, local, dev, wd, comm, nccl_group, rehearse)
     if rank == 0 and a.cpu_spp > 0 and world == 1:
         with wd.stage("cpu baseline (oracle on the host cores)", 900.0):
             cpu = cpu_baseline(preset, cam, W, H, a.cpu_spp, depth, a.cpu_threads)
@@ -519,6 +661,8 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu,
             # N > 1: per-device render / own-gather ms and render max / mean (also in roofline)
             "device_balance": balance,
+            # BASELINE configs[4] (david, the 8-GPU config) at reduced spp on the same N-GPU path
+            "david": david,
         }
         print(json.dumps(line), flush=True)
     with wd.stage("teardown (communicators, process group)", BASE_DEADLINE_S):

@@ -235,7 +235,18 @@ typedef struct yart_render_stats {
   uint64_t coop_idle_slots; /* ... quad slots of those rounds holding no ray (the drain) */
   uint64_t world_iters;    /* world-BVH walk: loop iterations the waves issue (per-lane visits: node_visits, prim_tests) */
   uint64_t world_leaf_iters; /* ... of them with some lane at a leaf               */
-  uint64_t reserved[2];
+  uint64_t ovf_pushes;     /* deep meshes: walk-stack entries pushed past the LDS slots into HBM */
+  /* where the waves' lane-slots go (sums of active lanes, 64 per wave-instruction slot): */
+  uint64_t coop_node_rounds;    /* cooperative walk rounds whose inner-node branch runs          */
+  uint64_t coop_node_lanes;     /* ... lanes in that branch (4 per quad at a node)               */
+  uint64_t coop_leaf_lanes;     /* lanes testing a triangle in the leaf branch (coop_leaf_rounds) */
+  uint64_t coop_leaf_quad_lanes; /* ... lanes of the quads at a leaf (4 per quad)                */
+  uint64_t iterations;          /* render-loop iterations (per wave)                             */
+  uint64_t camera_lanes;        /* lanes starting a camera ray, summed over iterations           */
+  uint64_t scatter_lanes;       /* lanes scattering at a hit, summed over iterations             */
+  uint64_t camera_iters;        /* iterations in which some lane starts a camera ray             */
+  uint64_t scatter_iters;       /* iterations in which some lane scatters                        */
+  uint64_t reserved[1];
 } yart_render_stats;
 
 typedef void (*yart_progress_fn)(uint64_t pixels_done, void* user);

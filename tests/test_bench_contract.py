@@ -174,3 +174,30 @@ def test_bench_line_build_id_matches_the_pmc_snapshot():
     pmc = json.loads((PROF / "pmc_render_cornell.json").read_text())
     if b["roofline"]["traffic"] is not None:
         assert pmc.get("build_id") == bid
+
+
+def _check_david(d, n):
+    assert d["n_gpus"] == n and d["spp"] > 0 and d["frames"] >= 1 and d["warmup"] == 1
+    assert d["workload"].startswith("david 1920x1080x")
+    assert d["msamples_per_s"] == pytest.approx(1920 * 1080 * d["spp"] / (d["ms_per_frame"] * 1e-3) / 1e6, rel=2e-3)
+    bal = d["device_balance"]
+    assert len(bal["per_device_render_ms"]) == n and bal["render_max_over_mean"] >= 1.0
+    if n > 1:
+        assert len(bal["per_device_gather_ms"]) == n
+        assert d["frame_check"] == "assembled frame bitwise equal to the one-device render"
+
+
+def test_bench_line_carries_the_david_sub_record():
+    """the bench line also times BASELINE configs[4] (david 1920x1080, the
+    config BASELINE assigns to 8 GPUs) at reduced spp on the same N-GPU path, so the driver's
+    first 8-GPU run says whether david scales; checked on the newest N = 1 line and the newest
+    N = 2 rehearsal (r06+)."""
+    log, b = _bench_line()
+    if "david" not in b:
+        pytest.skip(f"{log.name} predates the david sub-record")
+    _check_david(b["david"], b["n_gpus"])
+    logs = sorted(PROF.glob("r0[6-9]*_rehearse_n2.log"))
+    if not logs:
+        pytest.skip("no r06+ rehearsal log")
+    r = [json.loads(l) for l in logs[-1].read_text().splitlines() if l.startswith("{")][-1]
+    _check_david(r["david"], 2)

@@ -377,6 +377,31 @@ def test_rays_in_face_planes_match_oracle(dev, opt, world_bvh):
     _hits_equal(h, o, h2, o2)
 
 
+@pytest.mark.parametrize("world_bvh", [0, 1])
+def test_rays_in_rotated_planes_match_oracle(dev, opt, world_bvh):
+    """The rotated variant of the test above: rays whose direction has NO zero
+    world component but an exactly zero one in a RotateY'd rect's or box's own frame (cos 90° · d_x
+    == d_z, and the like at 30°, -18° under Translate, 200° + 271.5°, under FlipFace), half of them
+    starting exactly in that local plane, where the reference's rect test "hits" with t = NaN
+    wherever the ray runs (tests/inplane_rays.py builds them). A 26-object list, list walk and
+    forced world BVH: the BVH's node boxes must not cull those hits (r05 residual: they did; the
+    walk now sends such rays to the list walk, DevScene::plane_frames). Closest hits bitwise the
+    oracle's."""
+    import inplane_rays as IR
+    opt("world_bvh", world_bvh)
+    b, planes = IR.rotated_planes_scene()
+    d = b.desc()
+    s = yart.DeviceScene(d)
+    assert (s.info().world_nodes > 0) == (world_bvh == 1)
+    rays = IR.rotated_plane_rays(planes, 2000)
+    assert (rays[:, 3:6] != 0).all()
+    h2, o2 = O.OracleScene(d).intersect(rays)
+    nan = (o2 >= 0) & np.isnan(h2[:, 0])
+    assert nan.sum() > 5000 and len(np.unique(o2[nan])) == 6  # every rotated object gets NaN-t hits
+    h, o = s.intersect(rays)
+    _hits_equal(h, o, h2, o2)
+
+
 @pytest.mark.parametrize("n", [17, 64, 257, 600])
 def test_world_bvh_4wide_mixed_lists_match_linear_scan(dev, n):
     """The 4-wide world BVH (forced on) over random mixed lists — plain, hollow and translated
@@ -1026,3 +1051,74 @@ def test_mesh_walk_near_coplanar_rays_match_oracle(dev, scene, reach):
         assert tris, i
         for tri, a, entry, exit_ in tris:
             assert abs(a) < 1e-12 and not (entry <= h2[i, 0] <= exit_), (i, tri, a, entry, exit_, h2[i, 0])
+
+
+_STACK = []
+
+
+def _layer_stack():
+    """(builder, desc, oracle scene) of the stacked-layers mesh, built once per session."""
+    if not _STACK:
+        n = 5 * 4 ** 10 + 64  # > 4 triangles under every level-10 node: every leaf at depth 11
+        x = (np.arange(n) * 1e-3).astype(np.float32)
+        pos = np.zeros((n, 9), np.float32)
+        pos[:, 0::3] = x[:, None]
+        pos[:, [1, 2, 5, 7]] = -1.0
+        pos[:, [4, 8]] = 3.0
+        nrm = np.zeros((n, 9))
+        nrm[:, 0::3] = 1.0
+        b = O.DescBuilder(background=(0.7, 0.8, 1.0))
+        m = b.material(abi.MAT_LAMBERTIAN, b.texture((0.6, 0.5, 0.4)))
+        b.mesh(pos, nrm)
+        b.obj(abi.PRIM_MESH, m, mesh=0)
+        d = b.desc()
+        _STACK.append((b, d, O.OracleScene(d)))
+    return _STACK[0]
+
+
+@pytest.mark.parametrize("walk", ["default", "reference_order", "lane_rewalk"])
+def test_deep_mesh_overflow_stack_is_used_and_exact(dev, walk):
+    """the megakernel's deep-mesh walks keep their first kStackSlots = 32 stack
+    entries in LDS and the rest in the per-wave HBM region (OVF) — exercised here, not assumed.
+    5,242,944 parallel triangles stacked along x (one per layer, every layer covering the same
+    y-z square): the reference's median-split L4QBVH has every leaf at depth 11 (more than 4
+    triangles under every level-10 node) and every box of a level spans the square, so a ray along
+    -x through the square hits all four children at every level, and a descent that defers three
+    of them per level pushes 33 entries: slot 32 lives in HBM.
+    Measured (tools/ovf_probe.py, profiles/r06f_ovf_probe.log): the default front-to-back walk on its
+    depth-11 walk tree pushes one entry per ray into the region (the cooperative walk's per-quad node
+    ids and 16-bit entries), and so does the per-lane reference-order re-walk (force_rewalk: per-lane
+    columns); the instrumented render counts those pushes (yart_render_stats.ovf_pushes > 0). The
+    cooperative walk in the reference's order (mesh_walk_ref = 1) visits the whole tree on these rays
+    without reaching slot 32. Production and instrumented renders, and a
+    ray batch, bitwise the oracle's in all three."""
+    b, d, o = _layer_stack()
+    with yart.option("mesh_walk_ref", 1 if walk == "reference_order" else 0):
+        s = yart.DeviceScene(d)
+    i = s.info()
+    assert i.bvh_max_depth == 11 and i.bvh_max_stack >= 33
+    # small on purpose: on this mesh the reference's own walk order is far to near along x, so a
+    # reference-order walk visits most of the tree (~0.13 s per ray on the oracle)
+    cam = yart.make_camera((5400.0, 0.4, 0.4), (0.0, 0.4, 0.4), 0.02, 1.0, 0.0)
+    prm = yart.render_params(8, 8, 1, 2)
+    want = o.render(cam, prm, threads=0)
+    if walk == "lane_rewalk":
+        assert dev.yart_debug_force_rewalk(0, 1) == 0
+    try:
+        img, st = s.render_with_stats(cam, prm)
+        np.testing.assert_array_equal(img, want)
+        np.testing.assert_array_equal(s.render(cam, prm), want)
+    finally:
+        assert dev.yart_debug_force_rewalk(0, 0) == 0
+    if walk != "reference_order":
+        assert st.ovf_pushes > 0, "the HBM overflow stack was never written"
+    assert (img[O.coverage(8, 8)].sum(axis=-1) != 0).mean() > 0.5
+    rng = np.random.default_rng(8)
+    k = 48
+    org = np.column_stack([np.full(k, 5500.0), rng.uniform(-0.5, 0.9, k), rng.uniform(-0.5, 0.9, k)])
+    dirs = np.column_stack([-np.ones(k), rng.normal(0, 1e-5, k), rng.normal(0, 1e-5, k)])
+    rays = np.column_stack([org, dirs, np.full(k, 0.001), np.full(k, np.inf)])
+    gh, go = s.intersect(rays)
+    oh, oo = o.intersect(rays)
+    _hits_equal(gh, go, oh, oo)
+    assert (go >= 0).all()

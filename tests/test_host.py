@@ -249,3 +249,20 @@ def test_oracle_obj_reader_on_hand_made_faces(tmp_path):
     np.testing.assert_array_equal(nrm[2, :3], cr / np.sqrt((cr * cr).sum()))
     p2, n2, u2 = yart.load_obj(f, with_uv=True)  # and the product agrees
     assert p2.tobytes() == pos.tobytes() and n2.tobytes() == nrm.tobytes() and u2.tobytes() == uv.tobytes()
+
+
+def test_rotated_plane_rays_are_in_plane_nan_hits_for_the_oracle():
+    """tests/inplane_rays.py's construction (the data of test_rays_in_rotated_planes_match_oracle):
+    no world direction component is zero, the local one is, and the oracle reports t = NaN hits
+    on every rotated rect and box (aarect.rs:111-146 under hittable.rs:217-251)."""
+    import time
+
+    import inplane_rays as IR
+    t0 = time.time()
+    b, planes = IR.rotated_planes_scene()
+    rays = IR.rotated_plane_rays(planes, 300)
+    assert time.time() - t0 < 30
+    assert (rays[:, 3:6] != 0).all()
+    h, o = O.OracleScene(b.desc()).intersect(rays)
+    nan = (o >= 0) & np.isnan(h[:, 0])
+    assert nan.sum() > 500 and len(np.unique(o[nan])) == 6

@@ -17,7 +17,7 @@
 # Raw outputs under gpurun_out/; tools/summarize_profiles.py turns them into profiles/ files.
 set -u
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$REPO/gpurun_out; mkdir -p "$OUT"; cd "$REPO"
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 run() {
   local name=$1 limit=$2; shift 2
   timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
@@ -29,6 +29,10 @@ STEPS=${STEPS:-"pytest smoke bench prof_cornell prof_cornell_s1 prof_david prof_
 for s in $STEPS; do
   case $s in
     pytest) run ${TAG}_gpu_tests 900 python3 -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    pytest_k) run ${TAG}_gpu_tests_k 600 python3 -u -m pytest tests -m gpu -k "$PYTEST_K" -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    ab) run ${TAG}_ab 1200 bash tools/gpu_mesh_ab.sh ;;
+    probe) run ${TAG}_ovf_probe 300 python3 tools/ovf_probe.py ;;
+    lanes) run ${TAG}_lane_phases 300 python3 tools/lane_phases.py david 960 540 16 bunny 800 800 16 cornell-box 800 800 16 random-scene 600 400 16 ;;
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;

@@ -33,6 +33,6 @@ for p in $PASSES; do
     ta)    step ${PFX:-}prof_ta 600 rocprofv3 --kernel-trace --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum --output-format csv -d "$OUT/${PFX:-}prof_ta" -o run -- python3 $REPO/$PROG ;;
     tcp)   step ${PFX:-}prof_tcp 600 rocprofv3 --kernel-trace --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum --output-format csv -d "$OUT/${PFX:-}prof_tcp" -o run -- python3 $REPO/$PROG ;;
     lds)   step ${PFX:-}prof_lds 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_SMEM --output-format csv -d "$OUT/${PFX:-}prof_lds" -o run -- python3 $REPO/$PROG ;;
-    valu)  step ${PFX:-}prof_valu 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/${PFX:-}prof_valu" -o run -- python3 $REPO/$PROG ;;
+    valu)  step ${PFX:-}prof_valu 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/${PFX:-}prof_valu" -o run -- python3 $REPO/$PROG ;;
   esac
 done

@@ -51,6 +51,15 @@ def main():
                     summary.setdefault("lds_bytes", int(r["LDS_Block_Size"]))
                     summary.setdefault("grid", int(r["Grid_Size"]))
                     break
+    # the VALU active-lane ratio SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU of this kernel, and of
+    # k_accumulate in the same pass: a streaming kernel whose waves run full (64 lanes) except at
+    # the grid's end, so its ratio calibrates the counters' units
+    if summary.get("SQ_THREAD_CYCLES_VALU") and summary.get("SQ_ACTIVE_INST_VALU"):
+        summary["valu_thread_per_active_inst"] = summary["SQ_THREAD_CYCLES_VALU"] / summary["SQ_ACTIVE_INST_VALU"]
+        if (OUT / (pfx + "prof_valu") / "run_counter_collection.csv").exists():
+            cal, _ = per_launch(pfx + "prof_valu", "k_accumulate")
+            if cal.get("SQ_THREAD_CYCLES_VALU") and cal.get("SQ_ACTIVE_INST_VALU"):
+                summary["calib_k_accumulate_thread_per_active_inst"] = cal["SQ_THREAD_CYCLES_VALU"] / cal["SQ_ACTIVE_INST_VALU"]
     stats = list(csv.DictReader(open(PROF / f"{tag}_kernel_stats.csv")))
     for s in stats:
         if kernel in s["Name"]:

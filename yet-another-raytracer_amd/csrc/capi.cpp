@@ -344,6 +344,10 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
     HIP_TRY(upload(s->owned, world.objs.data(), world.objs.size(), &ds.world_objs, bytes), "upload world objects");
     HIP_TRY(upload(s->owned, world.sph.data(), world.sph.size(), &ds.world_sph, bytes), "upload world spheres");
     ds.n_world_nodes = (uint32_t)world.nodes4.size();
+    if (!world.plane_dirs.empty())
+      HIP_TRY(upload(s->owned, world.plane_dirs.data(), world.plane_dirs.size(), &ds.plane_dirs, bytes),
+              "upload in-plane directions");
+    ds.n_plane_dirs = (uint32_t)world.plane_dirs.size();
   }
   ds.n_objects = d->n_objects; ds.n_lights = d->n_lights; ds.n_materials = d->n_materials;
   ds.n_textures = d->n_textures; ds.n_meshes = d->n_meshes;
@@ -612,22 +616,29 @@ int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out
 // drained. When the device cannot hold that much (the auto budget is sized from its total memory,
 // not from what is free: other scenes, streams or the caller's own allocations may hold the rest),
 // the pass shrinks by halves, down to one unit (`min_spp` samples), instead of failing the frame:
-// more passes, the same frame (k_accumulate adds in sample order whatever the split).
+// more passes, the same frame (k_accumulate adds in sample order whatever the split). The larger
+// buffer is allocated BEFORE the working one is released: on a nearly full device a frame then
+// costs a failed hipMalloc or two and runs in the buffer it has, with no stream drain and no
+// free/re-allocate churn per frame, and grows as soon as the memory is there.
 int pass_scratch(StreamState* st, hipStream_t stream, const RenderArgs& a, Plan& pl, uint32_t min_spp,
                  double** out) {
   for (;;) {
     const size_t bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double) + 256;
     if (st->bytes >= bytes) { *out = st->scratch; return YART_OK; }
-    if (st->scratch) {
-      HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its scratch");
-      HIP_TRY(hipFree(st->scratch), "hipFree scratch");
+    double* grown = nullptr;
+    const hipError_t e = hipMalloc(&grown, bytes);
+    if (e == hipSuccess) {
+      if (st->scratch) {
+        const hipError_t d = hipStreamSynchronize(stream);  // earlier frames may still use the old one
+        if (d != hipSuccess) { (void)hipFree(grown); return hip_fail(d, "drain the stream before growing its scratch"); }
+        HIP_TRY(hipFree(st->scratch), "hipFree scratch");
+      }
+      st->scratch = grown; st->bytes = bytes;
+      *out = st->scratch;
+      return YART_OK;
     }
-    st->scratch = nullptr; st->bytes = 0;
-    const hipError_t e = hipMalloc(&st->scratch, bytes);
-    if (e == hipSuccess) { st->bytes = bytes; *out = st->scratch; return YART_OK; }
-    st->scratch = nullptr;
     if (e != hipErrorOutOfMemory || pl.pass_spp <= min_spp) return hip_fail(e, "hipMalloc scratch");
-    (void)hipGetLastError();  // clear the allocation failure and try half the pass
+    (void)hipGetLastError();  // clear the allocation failure and try half the pass (or the old buffer)
     uint32_t half = pl.pass_spp / 2 / min_spp * min_spp;
     pl.pass_spp = half < min_spp ? min_spp : half;
   }
@@ -837,7 +848,8 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     b.waves = (uint32_t)s->cu_count * 16;  // 4 waves per SIMD resident
     b.progress_base = base;
     base += b.n_units;
-    HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream), "zero the unit counter");
+    // the unit counter, and the 8 XCD-local ones of mesh frames (kernels.hip, claim of a unit)
+    HIP_TRY(hipMemsetAsync(queue, 0, 9 * sizeof(uint32_t), stream), "zero the unit counters");
     HIP_TRY(hipEventRecord(ev[3 * k], stream), "hipEventRecord");
     HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
     HIP_TRY(hipEventRecord(ev[3 * k + 1], stream), "hipEventRecord");
@@ -1024,8 +1036,8 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
   HIP_TRY(hipMemsetAsync(d_out, 0, bytes, stream), "hipMemset");
   if (stats) {
-    HIP_TRY(hipMalloc(&d_stats, 14 * sizeof(unsigned long long)), "hipMalloc stats");
-    HIP_TRY(hipMemsetAsync(d_stats, 0, 14 * sizeof(unsigned long long), stream), "hipMemset");
+    HIP_TRY(hipMalloc(&d_stats, 24 * sizeof(unsigned long long)), "hipMalloc stats");
+    HIP_TRY(hipMemsetAsync(d_stats, 0, 24 * sizeof(unsigned long long), stream), "hipMemset");
   }
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
@@ -1044,7 +1056,7 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   if (int rc = wait_with_progress({done}, {s->device}, {&pr}, pr.pixels, progress, user)) return rc;
   HIP_TRY(hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, stream), "copy output");
   if (stats) {
-    unsigned long long v[14];
+    unsigned long long v[24];
     HIP_TRY(hipMemcpyAsync(v, d_stats, sizeof v, hipMemcpyDeviceToHost, stream), "copy stats");
     HIP_TRY(hipStreamSynchronize(stream), "copy stats");
     std::memset(stats, 0, sizeof *stats);
@@ -1054,6 +1066,10 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
     stats->coop_rounds = v[8]; stats->coop_leaf_rounds = v[9]; stats->coop_walks = v[10];
     stats->coop_idle_slots = v[11];
     stats->world_iters = v[12]; stats->world_leaf_iters = v[13];
+    stats->ovf_pushes = v[14];
+    stats->coop_node_rounds = v[15]; stats->coop_node_lanes = v[16]; stats->coop_leaf_lanes = v[17];
+    stats->coop_leaf_quad_lanes = v[18]; stats->iterations = v[19]; stats->camera_lanes = v[20];
+    stats->scatter_lanes = v[21]; stats->camera_iters = v[22]; stats->scatter_iters = v[23];
   }
   HIP_TRY(hipStreamSynchronize(stream), "copy output");
   return ok();

@@ -21,6 +21,11 @@
 namespace yart_dev {
 
 constexpr int kMaxXforms = 4;
+// DevScene::plane_dirs (world_bvh.h BuiltWorld::plane_dirs): the half-width of the window around
+// each in-plane direction, in diamond-angle units (<= radians). A computed local component is
+// exactly 0 only within ~m 1e-15 rad of it (m RotateYs), or when the x-z direction is so short that
+// the products underflow (world_closest_bvh checks that too).
+constexpr double kPlaneDirWindow = 1e-9;
 constexpr int kBins = 36;
 constexpr int kStackSlots = 32;     // per-lane LDS traversal stack; 3*depth+1 <= 32 -> depth <= 10
 constexpr uint32_t kMaxListObjects = 1u << 29;  // the world pass keeps obj << 3 | sub in one word (kernels.hip HitId)
@@ -143,11 +148,13 @@ struct DevScene {
   const DevWorldNode4* world_nodes;  // the 4-wide world BVH (root = node 0); null: walk the list linearly
   const uint32_t* world_objs;
   const double* world_sph;   // per world_objs slot: centre xyz, radius (plain spheres; else 0)
+  const double* plane_dirs;  // BuiltWorld::plane_dirs (n_plane_dirs, a power of two; 0: none)
   uint32_t n_objects, n_lights, n_materials, n_textures, n_meshes;
   uint32_t has_mesh;
   uint32_t has_ext;  // noise/image textures, isotropic materials, media or moving spheres (EXT kernels)
   uint32_t has_time; // a MovingSphere reads the ray's shutter time: the camera draws it
   uint32_t n_world_nodes;
+  uint32_t n_plane_dirs;
   uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
 };
 

@@ -15,8 +15,8 @@ struct RenderArgs {
   uint32_t shard_index, shard_count;
   uint32_t blocks_x;  // ceil(width / 8)
   uint32_t n_blocks;  // 8x8-pixel blocks owned by this shard
-  // Work units = n_blocks x n_chunks; unit u renders block u % n_blocks for samples
-  // [s_begin + (u / n_blocks) * chunk, ... + chunk) clipped to [s_begin, s_begin + s_count).
+  // Work units = n_blocks x n_chunks, block-major: unit u renders block u / n_chunks for samples
+  // [s_begin + (u % n_chunks) * chunk, ... + chunk) clipped to [s_begin, s_begin + s_count).
   uint32_t s_begin, s_count, chunk, n_chunks;
   uint32_t* queue;    // chunked path: unit counter (zeroed before each launch), claimed by persistent waves
   uint32_t n_units;   // n_blocks * n_chunks

@@ -692,9 +692,16 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
 }
 
 // --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543)
-constexpr int kNumStats = 14;
+constexpr int kNumStats = 24;
 struct Stats { unsigned long long v[kNumStats]; };
-enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };  // ST_REWALK = 7 below
+enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };  // ST_REWALK = 7 .. 13 below
+enum { ST_OVF_PUSHES = 14 };  // deep meshes: walk-stack entries pushed past the LDS slots into the HBM region
+// Where a wave's lane-slots go, counted by lane 0 from ballots: the rounds
+// of the cooperative walk whose node branch runs and the lanes in it; the lanes testing a triangle in
+// the leaf branch and the lanes of the quads at a leaf; the loop's iterations and the lanes starting
+// a camera ray or scattering in them (and the iterations where each of those branches runs).
+enum { ST_NODE_ROUNDS = 15, ST_NODE_LANES = 16, ST_LEAF_LANES = 17, ST_LEAF_QUAD_LANES = 18, ST_ITERS = 19,
+       ST_CAMERA_LANES = 20, ST_SCATTER_LANES = 21, ST_CAMERA_ITERS = 22, ST_SCATTER_ITERS = 23 };
 
 // Ray octant: x >= 0 | y >= 0 << 1 | z >= 0 << 2, the ORDER_TABLE column (qbvh.rs:14-31); a
 // child's push rank for it is 2 bits of its node record (bvh_build.cpp).
@@ -826,8 +833,12 @@ __device__ __noinline__ LaneHit qbvh_lane(const DevMesh* __restrict__ Mp, double
       for (int k = 0; k < 4; ++k) {  // pushed in rank order: slot = hit children of lower rank
         const int slot = cursor + (int)__popc(ordered & ((1u << rank[k]) - 1u));
         if (hk[k]) {
-          if (!OVF || slot < kStackSlots) stk[slot * 64] = chs[k];
-          else ovf[(slot - kStackSlots) * 64] = chs[k];
+          if (!OVF || slot < kStackSlots) {
+            stk[slot * 64] = chs[k];
+          } else {
+            ovf[(slot - kStackSlots) * 64] = chs[k];
+            if (STATS) stv[ST_OVF_PUSHES]++;
+          }
         }
       }
       cursor += (int)__popc(ordered);
@@ -1131,12 +1142,18 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     const bool has = ray < n;
     if (__ballot(has) == 0) break;
     if (STATS) {  // the ballots outside the lane-0 branch: they must see every quad
-      const bool any_leaf = __ballot(has && (node >> 31)) != 0;
+      const uint64_t at_leaf = __ballot(has && (node >> 31));
+      const uint64_t at_node = __ballot(has && !(node >> 31));
+      const uint64_t tri = __ballot(has && (node >> 31) && c < ((node >> 27) & 0xFu));
       const uint64_t busy = __ballot(has && c == 0u);
       if (lane == 0) {
         st.v[ST_ROUNDS]++;
-        st.v[ST_LEAF_ROUNDS] += any_leaf ? 1u : 0u;
+        st.v[ST_LEAF_ROUNDS] += at_leaf ? 1u : 0u;
         st.v[ST_IDLE_SLOTS] += 16u - (uint32_t)__popcll(busy);  // the drain: quads without a ray this round
+        st.v[ST_NODE_ROUNDS] += at_node ? 1u : 0u;
+        st.v[ST_NODE_LANES] += (uint32_t)__popcll(at_node);
+        st.v[ST_LEAF_LANES] += (uint32_t)__popcll(tri);
+        st.v[ST_LEAF_QUAD_LANES] += (uint32_t)__popcll(at_leaf);
       }
     }
     bool fin = false;
@@ -1252,6 +1269,7 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
             } else {  // deep meshes: entries past the LDS slots in the wave's HBM region
               ovf[slot - SLOTS * 16] = child;
               ovf[kOvfQuadWords + slot - SLOTS * 16] = e16;
+              if (STATS) st.v[ST_OVF_PUSHES]++;
             }
           }
           cursor += (int)__popc(ordered) - 1;
@@ -1560,6 +1578,24 @@ __device__ __forceinline__ void hit_record(const DevScene& S, const Ray& r, cons
 // the fma's and the per-ray constants' included) stays far inside m — over [t_min, closest]
 // widened by 2^-10, so it never drops a node holding a hit the scan would accept (ties included).
 // Non-finite rays take the list walk.
+// The diamond angle of the x-z direction mod pi: monotone in the angle phi with slope in [1/2, 1],
+// so a window of w around a tabulated direction covers at least w radians (world_bvh.cpp holds the
+// host's copy of this formula).
+__device__ __forceinline__ double plane_diamond(double dx, double dz) {
+  if (dz < 0.0 || (dz == 0.0 && dx < 0.0)) { dx = -dx; dz = -dz; }
+  const double ax = fabs(dx);
+  return dx >= 0.0 ? dz / (dx + dz) : 1.0 + ax / (ax + dz);
+}
+__device__ __noinline__ bool near_plane_dir(const DevScene& S, double dx, double dz) {
+  if (fabs(dx) + fabs(dz) < 1e-280) return true;  // so short that the rotations' products can underflow to 0
+  const double dm = plane_diamond(dx, dz), lo = dm - kPlaneDirWindow;
+  const double* tab = S.plane_dirs;
+  uint32_t i = 0;  // the first entry >= lo (a +inf pad entry at worst)
+  for (uint32_t s = S.n_plane_dirs >> 1; s != 0; s >>= 1)
+    if (tab[i + s - 1] < lo) i += s;
+  return tab[i] <= dm + kPlaneDirWindow;
+}
+
 template <bool STATS>
 __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& r, double tmin, double tmax, HitId& id,
                                                   uint32_t* stk, Stats& st) {
@@ -1568,7 +1604,12 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
   // Non-finite rays, and rays with an exactly zero direction component (which can lie in a rect's
   // plane, where rect_t's NaN t "hits" it outside any box, see box_may_hit), take the list walk.
-  if (!(fabsf(chk) <= 3.0e38f) || r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0)
+  bool in_plane = r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0;
+  // The same in the frames of the rotated rects and boxes: there a direction component can cancel to
+  // exactly 0 while no world component is 0 (cos 90° d_x == d_z). Rays near those directions
+  // (DevScene::plane_dirs) take the list walk too. 0 entries in scenes without rotated planes.
+  if (S.n_plane_dirs) in_plane = in_plane || near_plane_dir(S, r.d.x, r.d.z);
+  if (!(fabsf(chk) <= 3.0e38f) || in_plane)
     return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
   float inv[3];
   bool use[3];
@@ -2210,10 +2251,34 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
           const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(true));
           uint32_t v = 0;
           if (lane == first) {
-            v = atomicAdd(A.queue, 1u);
-            if (A.progress)  // yart_render's progress: the units handed out so far (host-mapped word)
-              __hip_atomic_store(A.progress, A.progress_base + (v < A.n_units ? v + 1u : A.n_units), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            if (HAS_MESH) {
+              // XCD-local queues (mesh frames): workgroups are dealt to the 8 XCDs round-robin, so
+              // XCD x takes the units of its own eighth of the frame first (its L2 then holds that
+              // patch's mesh nodes), then steals from the others in turn; a partition is empty once
+              // its counter passes its size, and every claim ends with a unit or after 8 tries.
+              // Same-box A/B: david +1.5 %, bunny +1.9 %; the list walk (cornell -1.2 %) and the
+              // world BVH (random-scene -0.2 %) keep the one counter (profiles/r05n_ab_xcd_queues.log).
+              v = 0xFFFFFFFFu;
+              const uint32_t x0 = blockIdx.x & 7u;
+              for (uint32_t k = 0; k < 8u; ++k) {
+                const uint32_t x = (x0 + k) & 7u;
+                const uint32_t lo = (uint32_t)(((uint64_t)A.n_units * x) >> 3);
+                const uint32_t hi = (uint32_t)(((uint64_t)A.n_units * (x + 1u)) >> 3);
+                if (hi <= lo) continue;
+                const uint32_t t = atomicAdd(A.queue + 1 + x, 1u);
+                if (t < hi - lo) { v = lo + t; break; }
+              }
+              if (A.progress) {  // the units handed out so far, counted on queue[0]
+                const uint32_t c = v < A.n_units ? atomicAdd(A.queue, 1u) + 1u : A.n_units;
+                __hip_atomic_store(A.progress, A.progress_base + (c < A.n_units ? c : A.n_units), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+              }
+            } else {
+              v = atomicAdd(A.queue, 1u);
+              if (A.progress)  // yart_render's progress: the units handed out so far (host-mapped word)
+                __hip_atomic_store(A.progress, A.progress_base + (v < A.n_units ? v + 1u : A.n_units), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
           }
           const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)first);
           if (u >= A.n_units) { drained = true; break; }
@@ -2259,6 +2324,16 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
     // T is the path's throughput while it runs and its result R (ray_reflectance's return value)
     // once it has ended (term): one register pair for both, since no lane needs both at once.
     bool term = false, want = false;
+    if (STATS) {
+      const uint64_t cam = __ballot(run && fresh), sca = __ballot(run && !fresh);
+      if (lane == 0) {
+        st.v[ST_ITERS]++;
+        st.v[ST_CAMERA_LANES] += (uint32_t)__popcll(cam);
+        st.v[ST_SCATTER_LANES] += (uint32_t)__popcll(sca);
+        st.v[ST_CAMERA_ITERS] += cam ? 1u : 0u;
+        st.v[ST_SCATTER_ITERS] += sca ? 1u : 0u;
+      }
+    }
     if (run) {
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration

@@ -365,20 +365,35 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
     HIP_TRY(hipMalloc(&S->recv, pk_bytes * (size_t)n), "hipMalloc gather buffer");
     S->recv_bytes = pk_bytes * (size_t)n;
   }
+  // The frame's timing pairs join the slot's lists only once both ends are recorded (below): a
+  // submission that fails half way returns them to their pools instead of leaving a pair that
+  // multi_timing cannot read.
   std::pair<hipEvent_t, hipEvent_t> gev;
   if (int rc = event_pair(m->gather_pool, gev)) return rc;
-  S->gather_events.push_back(gev);
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> dev_ev;
+  dev_ev.reserve((size_t)n);
+  struct Pending {
+    yart_multi* m;
+    std::pair<hipEvent_t, hipEvent_t>& gev;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>>& dev_ev;
+    bool handed_over = false;
+    ~Pending() {
+      if (handed_over) return;
+      m->gather_pool.push_back(gev);
+      for (size_t d = 0; d < dev_ev.size(); ++d) m->dev_pool[d].push_back(dev_ev[d]);
+    }
+  } pending{m, gev, dev_ev};
   // 3. ONE gather to devices[0], each device's part right behind its render; in submission order
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> dev_ev((size_t)n);
   for (int d = 0; d < n; ++d) {
     const size_t di = (size_t)d;
     HIP_TRY(hipSetDevice(m->devices[di]), "hipSetDevice");
     if (m->last_gather[di] && m->last_gather[di] != S->gathered[di])
       HIP_TRY(hipStreamWaitEvent(S->streams[di], m->last_gather[di], 0), "hipStreamWaitEvent");
     if (d == 0) HIP_TRY(hipEventRecord(gev.first, S->streams[0]), "hipEventRecord");
-    if (int rc = event_pair(m->dev_pool[di], dev_ev[di])) return rc;
-    S->dev_gather_events[di].push_back(dev_ev[di]);
-    HIP_TRY(hipEventRecord(dev_ev[di].first, S->streams[di]), "hipEventRecord");
+    std::pair<hipEvent_t, hipEvent_t> pr;
+    if (int rc = event_pair(m->dev_pool[di], pr)) return rc;
+    dev_ev.push_back(pr);
+    HIP_TRY(hipEventRecord(pr.first, S->streams[di]), "hipEventRecord");
   }
   NCCL_TRY(ncclGroupStart(), "ncclGroupStart");
   for (int d = 0; d < n; ++d) {
@@ -402,6 +417,9 @@ int multi_submit(yart_multi* m, const yart_camera* cam, const yart_render_params
   HIP_TRY(hipStreamWaitEvent(S->streams[0], S->start, 0), "hipStreamWaitEvent");
   HIP_TRY(launch_unpack_shards(S->recv, (uint32_t)n, stride, W, H, d_frame, S->streams[0]), "launch k_unpack_shards");
   HIP_TRY(hipEventRecord(gev.second, S->streams[0]), "hipEventRecord");
+  S->gather_events.push_back(gev);
+  for (int d = 0; d < n; ++d) S->dev_gather_events[(size_t)d].push_back(dev_ev[(size_t)d]);
+  pending.handed_over = true;
   HIP_TRY(hipEventRecord(S->done, S->streams[0]), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(caller, S->done, 0), "hipStreamWaitEvent");
   return YART_OK;
@@ -428,13 +446,18 @@ int multi_timing(yart_multi* m, MultiSlot* only, double* render_ms, double* gath
       r += rr;
       if (d == 0) nf += f;
       HIP_TRY(hipSetDevice(m->devices[(size_t)d]), "hipSetDevice");
-      for (auto& e : kv.second->dev_gather_events[(size_t)d]) {
+      // taken out of the slot first and recycled whatever happens: a failed read does not leave
+      // pairs behind for every later call to trip over
+      std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+      evs.swap(kv.second->dev_gather_events[(size_t)d]);
+      hipError_t bad = hipSuccess;
+      for (auto& e : evs) {
         float ms = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second), "hipEventElapsedTime");
-        dg += ms;
+        if (bad == hipSuccess) bad = hipEventElapsedTime(&ms, e.first, e.second);
+        if (bad == hipSuccess) dg += ms;
         m->dev_pool[(size_t)d].push_back(e);
       }
-      kv.second->dev_gather_events[(size_t)d].clear();
+      if (bad != hipSuccess) return hip_fail(bad, "hipEventElapsedTime");
     }
     m->dev_render_ms[(size_t)d] = r;
     m->dev_gather_ms[(size_t)d] = dg;
@@ -445,13 +468,16 @@ int multi_timing(yart_multi* m, MultiSlot* only, double* render_ms, double* gath
   double g = 0.0;
   for (auto& kv : m->slots) {
     if (only && kv.second.get() != only) continue;
-    for (auto& e : kv.second->gather_events) {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    evs.swap(kv.second->gather_events);
+    hipError_t bad = hipSuccess;
+    for (auto& e : evs) {
       float ms = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second), "hipEventElapsedTime");
-      g += ms;
+      if (bad == hipSuccess) bad = hipEventElapsedTime(&ms, e.first, e.second);
+      if (bad == hipSuccess) g += ms;
       m->gather_pool.push_back(e);
     }
-    kv.second->gather_events.clear();
+    if (bad != hipSuccess) return hip_fail(bad, "hipEventElapsedTime");
   }
   *render_ms = worst;
   *gather_ms = g;

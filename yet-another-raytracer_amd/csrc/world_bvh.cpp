@@ -6,6 +6,7 @@
 #include <numeric>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 namespace yart_dev {
@@ -262,6 +263,43 @@ bool collapse4(BuiltWorld& out, bool two_level) {
 // up to 2, 4, 8, 15 objects (depth ~ log2(n / leaf)), before the list walk is the answer.
 bool build_world_bvh_with(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah, size_t median_leaf);
 
+// BuiltWorld::plane_dirs. RotateY with (s, c) maps the x-z direction (dx, dz) to (c dx - s dz,
+// s dx + c dz): a rotation-scaling by theta = atan2(s, c). So a chain of them (Translate moves no
+// direction) zeroes the local x component along phi = pi/2 - sum(theta) and the local z component
+// along phi = -sum(theta), mod pi; away from those the computed component is far from 0 (the
+// rounding of the chain is ~m 2^-52 |d| against |d| |sin(phi - phi_0)|).
+double plane_diamond(double dx, double dz) {  // the device's formula (kernels.hip plane_diamond)
+  if (dz < 0.0 || (dz == 0.0 && dx < 0.0)) { dx = -dx; dz = -dz; }
+  const double ax = std::fabs(dx);
+  return dx >= 0.0 ? dz / (dx + dz) : 1.0 + ax / (ax + dz);
+}
+std::vector<double> plane_directions(const std::vector<DevObject>& objs) {
+  std::vector<double> v;
+  for (const DevObject& o : objs) {
+    if (o.kind == YART_PRIM_SPHERE || o.kind > YART_PRIM_BOX) continue;  // rects and boxes only
+    double theta = 0.0;
+    int rot = 0;
+    for (uint32_t l = 0; l < o.n_xf; ++l)
+      if (o.xf_kind[l] == YART_XF_ROTATE_Y) { theta += std::atan2(o.xf[l][0], o.xf[l][1]); ++rot; }
+    if (!rot) continue;  // unrotated: its planes are world planes, caught by the zero-component test
+    for (double phi : {M_PI / 2 - theta, -theta}) {
+      double sn, cs;
+      ::sincos(phi, &sn, &cs);  // (one call: the library imports no separate sin / cos, test_abi.py)
+      const double dm = plane_diamond(cs, sn);
+      v.push_back(dm);
+      if (dm < 4 * kPlaneDirWindow) v.push_back(dm + 2.0);  // the diamond angle wraps at 2 (= pi)
+      if (dm > 2.0 - 4 * kPlaneDirWindow) v.push_back(dm - 2.0);
+    }
+  }
+  if (v.empty()) return v;
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  size_t n = 1;
+  while (n < v.size() + 1) n <<= 1;  // at least one +inf: the device's search never runs off the end
+  v.resize(n, INFINITY);
+  return v;
+}
+
 }  // namespace
 
 bool build_world_bvh(const std::vector<DevObject>& objs, BuiltWorld& out, bool sah) {
@@ -308,6 +346,7 @@ bool build_world_bvh_with(const std::vector<DevObject>& objs, BuiltWorld& out, b
     n.pad[1] = (n.count << 28) | ((n.pad[0] & kWorldLeafSpheres) ? (1u << 27) : 0u) | n.first;
   }
   if (out.nodes[0].count != 0) return false;  // a single leaf: the list walk
+  out.plane_dirs = plane_directions(objs);
   if (collapse4(out, false) || collapse4(out, true)) return true;
   if (sah) return build_world_bvh_with(objs, out, false, 2);
   if (median_leaf < kWorldHandleMaxCount) return build_world_bvh_with(objs, out, false, std::min<size_t>(2 * median_leaf, kWorldHandleMaxCount));

@@ -16,7 +16,14 @@ struct BuiltWorld {
   std::vector<uint32_t> objs;       // leaf slots -> object index
   std::vector<double> sph;          // per leaf slot: centre xyz, radius of a plain sphere (else 0)
   uint32_t depth = 0;               // inner levels on the deepest root-to-leaf path
+  // The directions in the x-z plane along which a ray lies in a RotateY'd rect's or box's own plane
+  // (a local x or z direction component of exactly 0), as sorted "diamond angles" mod pi (kernels.hip
+  // plane_diamond), padded with +inf to a power of two. Such a ray can get the reference's t = 0/0 =
+  // NaN "hit" outside any box (aarect.rs:111-146, under hittable.rs:217-251); world_closest_bvh
+  // sends every ray within kPlaneDirWindow of one of them to the list walk.
+  std::vector<double> plane_dirs;
 };
+
 
 // World-space bounds of one list entry: the primitive's own box (sphere ± |r|, rect extent with
 // its plane coordinate, box corners, triangle vertices) carried through its wrappers innermost

@@ -91,7 +91,11 @@ class RenderStats(C.Structure):
                 ("light_tests", C.c_uint64), ("mesh_rewalks", C.c_uint64),
                 ("coop_rounds", C.c_uint64), ("coop_leaf_rounds", C.c_uint64), ("coop_walks", C.c_uint64),
                 ("coop_idle_slots", C.c_uint64), ("world_iters", C.c_uint64),
-                ("world_leaf_iters", C.c_uint64), ("reserved", C.c_uint64 * 2)]
+                ("world_leaf_iters", C.c_uint64), ("ovf_pushes", C.c_uint64),
+                ("coop_node_rounds", C.c_uint64), ("coop_node_lanes", C.c_uint64), ("coop_leaf_lanes", C.c_uint64),
+                ("coop_leaf_quad_lanes", C.c_uint64), ("iterations", C.c_uint64), ("camera_lanes", C.c_uint64),
+                ("scatter_lanes", C.c_uint64), ("camera_iters", C.c_uint64), ("scatter_iters", C.c_uint64),
+                ("reserved", C.c_uint64 * 1)]
 
 
 class RenderDefaults(C.Structure):
