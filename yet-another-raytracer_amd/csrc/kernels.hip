@@ -1645,20 +1645,23 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   int cursor = 0;
   uint32_t kk = 0;  // the next sphere of the current leaf
   for (;;) {
-    const uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
+    uint32_t count = hnd >> 28, first = hnd & (kWorldHandleFirstMask - 1u);
     if (STATS) {  // SIMT efficiency of the per-lane walk: iterations the wave issues (lane visits: ST_NODES, ST_PRIM)
       const uint64_t on = __ballot(true), lf = __ballot(count != 0u);
       if (__lane_id() == (uint32_t)__builtin_ctzll(on)) { st.v[ST_WORLD_ITERS]++; st.v[ST_WORLD_LEAF_ITERS] += lf ? 1u : 0u; }
     }
-    bool pop = true;
-    if (count && ((hnd >> 27) & 1u)) {
-      // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
-      // object records and the kind switch; the same sphere_t on the same values
-      // ONE sphere per loop iteration (the lane stays on the leaf until its spheres are done), not the
-      // whole leaf in an inner loop: an iteration in which some lane sits at a 4-sphere leaf then
-      // costs the wave one sphere test, not four (r05: random-scene +1.7-1.8 %, same box, bitwise;
-      // profiles/r05_ab_world_step1.log). The order of the tests, and so the answer, is unchanged.
-      {
+    // An iteration is a leaf step (lanes at a leaf) followed by an inner-node step (lanes at an inner
+    // node, including those whose leaf step just finished the leaf and popped one): a lane leaving a
+    // leaf steps its next node in the same iteration instead of the next. Each lane takes the same
+    // steps in the same order, so the answer is unchanged; the wave runs fewer iterations.
+    if (count) {
+      bool done = true;
+      if ((hnd >> 27) & 1u) {
+        // a leaf of plain spheres: the compact records (32 B each, one load pair) instead of the
+        // object records and the kind switch; the same sphere_t on the same values. ONE sphere per
+        // iteration (the lane stays on the leaf until its spheres are done), not the whole leaf in
+        // an inner loop: an iteration in which some lane sits at a 4-sphere leaf then costs the wave
+        // one sphere test, not four (r05: random-scene +1.7-1.8 %, profiles/r05_ab_world_step1.log).
         const uint32_t k = kk;
         const uint32_t i = S.world_objs[first + k];
         const double* sp = S.world_sph + 4 * (size_t)(first + k);
@@ -1670,24 +1673,31 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
           found = true;
         }
         kk = k + 1u;
-        if (kk < count) pop = false;  // the leaf's next sphere in the next iteration
+        if (kk < count) done = false;  // the leaf's next sphere in the next iteration
         else kk = 0u;
-      }
-    } else if (count) {
-      for (uint32_t k = 0; k < count; ++k) {
-        const uint32_t i = S.world_objs[first + k];
-        const DevObject& ob = S.objects[i];
-        const Ray lr = to_local(ob, ob.n_xf, r);
-        double t, u = 0.0, v = 0.0;
-        uint32_t sub = 0;
-        if (prim_t<false, STATS>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
-            (!found || t < closest || (i << 3) > who)) {
-          closest = t;
-          who = (i << 3) | sub;
-          found = true;
+      } else {
+        for (uint32_t k = 0; k < count; ++k) {
+          const uint32_t i = S.world_objs[first + k];
+          const DevObject& ob = S.objects[i];
+          const Ray lr = to_local(ob, ob.n_xf, r);
+          double t, u = 0.0, v = 0.0;
+          uint32_t sub = 0;
+          if (prim_t<false, STATS>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
+              (!found || t < closest || (i << 3) > who)) {
+            closest = t;
+            who = (i << 3) | sub;
+            found = true;
+          }
         }
       }
-    } else {
+      if (done) {  // the next handle: stepped below if it is an inner node, else next iteration
+        if (cursor == 0) break;
+        cursor--;
+        hnd = stk[cursor * 64];
+      }
+    }
+    if ((hnd >> 28) == 0u) {  // an inner node
+      first = hnd & (kWorldHandleFirstMask - 1u);
       float thi = (float)closest;
       thi = thi + fabsf(thi) * 0x1p-10f;
       const gfloat4p N = nodes + 8 * (size_t)first;
@@ -1732,13 +1742,11 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
         if (key[2] < INFINITY) stk[(cursor++) * 64] = hc[2];
         if (key[1] < INFINITY) stk[(cursor++) * 64] = hc[1];
         hnd = hc[0];
-        pop = false;
+      } else {
+        if (cursor == 0) break;
+        cursor--;
+        hnd = stk[cursor * 64];
       }
-    }
-    if (pop) {
-      if (cursor == 0) break;
-      cursor--;
-      hnd = stk[cursor * 64];
     }
   }
   id.obj = who >> 3; id.sub = who & 7u;
