@@ -1142,81 +1142,24 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     const bool has = ray < n;
     if (__ballot(has) == 0) break;
     if (STATS) {  // the ballots outside the lane-0 branch: they must see every quad
-      const uint64_t at_leaf = __ballot(has && (node >> 31));
       const uint64_t at_node = __ballot(has && !(node >> 31));
-      const uint64_t tri = __ballot(has && (node >> 31) && c < ((node >> 27) & 0xFu));
       const uint64_t busy = __ballot(has && c == 0u);
       if (lane == 0) {
         st.v[ST_ROUNDS]++;
-        st.v[ST_LEAF_ROUNDS] += at_leaf ? 1u : 0u;
         st.v[ST_IDLE_SLOTS] += 16u - (uint32_t)__popcll(busy);  // the drain: quads without a ray this round
         st.v[ST_NODE_ROUNDS] += at_node ? 1u : 0u;
         st.v[ST_NODE_LANES] += (uint32_t)__popcll(at_node);
-        st.v[ST_LEAF_LANES] += (uint32_t)__popcll(tri);
-        st.v[ST_LEAF_QUAD_LANES] += (uint32_t)__popcll(at_leaf);
       }
     }
     bool fin = false;
     if (has) {  // quad-uniform from here on
-      bool popped = false;  // the inner step set the next node itself
-      if (node >> 31) {
-        uint32_t count = (node >> 27) & 0xFu;
-        const uint32_t first = node & ((1u << 27) - 1u);
-#ifdef YART_WALK_CHECK
-        if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
-#endif
-        // A candidate's key orders equal t's as the reference visits them: front to back (either
-        // tree) by (the reference leaf's depth-first rank for this octant, lane in that leaf) and
-        // the quad lane in the low bits; in the reference's own order the lower lane of the leaf.
-        // t and key take their no-candidate values in one select after the test: set up front,
-        // the defaults were copied again at every exit of the short-circuited test.
-        double tt, u, v;
-        uint32_t kk, id, li = 0u;  // li is read across the quad (ds_bpermute): defined in every lane
-        bool cand = false;
-        if (c < count) {
-          const gfloat4p R = leaves + kRecF4 * (size_t)(first + c);
-          uint32_t ln, so;
-          const TriF64 g = tri_load(R, li, ln, so);  // li: the record's reference leaf
-#ifdef YART_WALK_CHECK
-          if (li >= M.n_leaves) { walk_fault(2u); li = 0u; }
-#endif
-          // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
-          // back: the tie goes to the reference's visiting order)
-          const CoopRay& s = rays[ray];
-          const double ro[3] = {s.o[0], s.o[1], s.o[2]}, rd[3] = {s.d[0], s.d[1], s.d[2]};
-          if (leaf_tri_hit(g, ro, rd, tmin, s.tmax, tt, u, v) && (tt < tb || (f2b && tt == tb))) {
-            cand = true;
-            id = so;  // sorted index: the normal table's row
-            kk = f2b ? (aux[li].rank[pos] << 4) | (ln << 2) | c : c;
-          }
-        }
-        double t = cand ? tt : INFINITY;
-        uint32_t key = cand ? kk : 0xFFFFFFFFu;
-        if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
-        quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
-        quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
-        if (key != 0xFFFFFFFFu) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
-          const uint32_t w = key & 3u;
-          // t == tb only front to back with a best already held: the reference's order decides
-          const bool better = t < tb || key < bkey;
-          li = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane & ~3u) | w) << 2), (int)li);  // the winner's leaf
-          if (better) {
-            tb = t; fnd = true; bleaf = li; bkey = key;
-            if (c == w) {
-              CoopRay& s = rays[ray];
-              coop_put_d(&s.c32[0], t); coop_put_d(&s.c32[2], u); coop_put_d(&s.c32[4], v);
-              s.inv32[0] = __uint_as_float(id);
-              s.inv32[1] = __uint_as_float(1u);
-            }
-            if (f2b) {
-              const double lim = t * (1.0 + kF2bMargin), tin = rays[ray].tmax;
-              const double teff = lim < tin ? lim : tin;
-              teff32 = (float)(teff + teff * 0x1p-20);
-              bound = (float)lim;
-            }
-          }
-        }
-      } else {
+      // A round is an inner-node step (quads at a node) followed by a leaf step (quads at a leaf,
+      // including those whose node step just descended into one), then one pop for the quads whose
+      // step ended without a next node: a quad descending into a leaf tests it in the same round
+      // instead of the next. Each quad takes the same steps in the same order, so the walk's answer
+      // is unchanged; the wave runs fewer rounds.
+      bool pop_now = false;
+      if (!(node >> 31)) {
 #ifdef YART_WALK_CHECK
         if (node >= M.n_nodes) { walk_fault(4u); node = root; }
 #endif
@@ -1277,10 +1220,76 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
           if (cursor >= (OVF ? kMaxStackSlots : SLOTS)) cursor = (OVF ? kMaxStackSlots : SLOTS) - 1;
 #endif
           node = nx;
-          popped = true;
+        } else {
+          pop_now = true;
         }
       }
-      if (!popped) {
+      if (!pop_now && (node >> 31)) {
+        if (STATS) {
+          const uint64_t lq = __ballot(true), lt = __ballot(c < ((node >> 27) & 0xFu));
+          if (lane == (uint32_t)__builtin_ctzll(lq)) {
+            st.v[ST_LEAF_ROUNDS]++; st.v[ST_LEAF_QUAD_LANES] += (uint32_t)__popcll(lq); st.v[ST_LEAF_LANES] += (uint32_t)__popcll(lt);
+          }
+        }
+        uint32_t count = (node >> 27) & 0xFu;
+        const uint32_t first = node & ((1u << 27) - 1u);
+#ifdef YART_WALK_CHECK
+        if (first + count > M.n_recs || count == 0 || count > 4) { walk_fault(1u); count = 0; }
+#endif
+        // A candidate's key orders equal t's as the reference visits them: front to back (either
+        // tree) by (the reference leaf's depth-first rank for this octant, lane in that leaf) and
+        // the quad lane in the low bits; in the reference's own order the lower lane of the leaf.
+        // t and key take their no-candidate values in one select after the test: set up front,
+        // the defaults were copied again at every exit of the short-circuited test.
+        double tt, u, v;
+        uint32_t kk, id, li = 0u;  // li is read across the quad (ds_bpermute): defined in every lane
+        bool cand = false;
+        if (c < count) {
+          const gfloat4p R = leaves + kRecF4 * (size_t)(first + c);
+          uint32_t ln, so;
+          const TriF64 g = tri_load(R, li, ln, so);  // li: the record's reference leaf
+#ifdef YART_WALK_CHECK
+          if (li >= M.n_leaves) { walk_fault(2u); li = 0u; }
+#endif
+          // candidates: t in [t_min, t_max_in) and nearer than the best, or as near (front to
+          // back: the tie goes to the reference's visiting order)
+          const CoopRay& s = rays[ray];
+          const double ro[3] = {s.o[0], s.o[1], s.o[2]}, rd[3] = {s.d[0], s.d[1], s.d[2]};
+          if (leaf_tri_hit(g, ro, rd, tmin, s.tmax, tt, u, v) && (tt < tb || (f2b && tt == tb))) {
+            cand = true;
+            id = so;  // sorted index: the normal table's row
+            kk = f2b ? (aux[li].rank[pos] << 4) | (ln << 2) | c : c;
+          }
+        }
+        double t = cand ? tt : INFINITY;
+        uint32_t key = cand ? kk : 0xFFFFFFFFu;
+        if (STATS && c == 0) { st.v[ST_LEAVES]++; st.v[ST_LEAF_TRIS] += count; }
+        quad_min<0xB1>(t, key);  // quad_perm [1,0,3,2]
+        quad_min<0x4E>(t, key);  // quad_perm [2,3,0,1]
+        if (key != 0xFFFFFFFFu) {  // the winning lane keeps its u, v, triangle; the quad keeps t and who
+          const uint32_t w = key & 3u;
+          // t == tb only front to back with a best already held: the reference's order decides
+          const bool better = t < tb || key < bkey;
+          li = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane & ~3u) | w) << 2), (int)li);  // the winner's leaf
+          if (better) {
+            tb = t; fnd = true; bleaf = li; bkey = key;
+            if (c == w) {
+              CoopRay& s = rays[ray];
+              coop_put_d(&s.c32[0], t); coop_put_d(&s.c32[2], u); coop_put_d(&s.c32[4], v);
+              s.inv32[0] = __uint_as_float(id);
+              s.inv32[1] = __uint_as_float(1u);
+            }
+            if (f2b) {
+              const double lim = t * (1.0 + kF2bMargin), tin = rays[ray].tmax;
+              const double teff = lim < tin ? lim : tin;
+              teff32 = (float)(teff + teff * 0x1p-20);
+              bound = (float)lim;
+            }
+          }
+        }
+        pop_now = true;
+      }
+      if (pop_now) {
         for (;;) {  // front to back: entries whose box begins beyond the bound are dropped
           if (cursor == 0) { fin = true; break; }
           cursor -= 1;
