@@ -40,8 +40,12 @@ def main():
     PROF.mkdir(exist_ok=True)
     shutil.copy(OUT / (pfx + "prof_trace") / "run_kernel_stats.csv", PROF / f"{tag}_kernel_stats.csv")
     summary = {"kernel": kernel, "source": "tools/profile.sh (rocprofv3 --pmc, one counter block per pass)"}
+    t_trace = (OUT / (pfx + "prof_trace") / "run_kernel_trace.csv").stat().st_mtime
     for p in ("prof_fetch", "prof_write", "prof_valu", "prof_stall", "prof_mix", "prof_mem", "prof_icache"):
-        if (OUT / (pfx + p) / "run_counter_collection.csv").exists():
+        f = OUT / (pfx + p) / "run_counter_collection.csv"
+        # only the passes of the same run as the trace (a pass left under gpurun_out/ by an earlier
+        # call would otherwise overwrite this run's counters)
+        if f.exists() and abs(f.stat().st_mtime - t_trace) < 1800:
             v, rows = per_launch(pfx + p, kernel)
             summary.update(v)
             for r in rows:
