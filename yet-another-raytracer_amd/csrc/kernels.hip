@@ -139,11 +139,12 @@ __device__ __forceinline__ bool flagged(const Ieee&) { return false; }
 // 1,514, david (mesh) 243.4 vs 243.3. So Fast ran where it won, the plain list kernel, and the
 // others kept Ieee (the second copy of the block costs them registers). Re-measured in r05 on the
 // world-BVH kernel after its walk changes: +0.2..+2.1 % over five same-box runs
-// (profiles/r05_ab_bvh_fast_policy_*.log), so the world-BVH kernel runs Fast too; the mesh and EXT
-// kernels keep Ieee.
+// (profiles/r05_ab_bvh_fast_policy_*.log), so the world-BVH kernel runs Fast too. Re-measured in r06 on
+// the mesh kernel after its walk changes: david 1920x1080x64 +0.7 %, bunny 800x800x512 +1.3 %, david
+// 960x540x16 +1.2 % (profiles/r06k_ab_mesh_fast_policy.log), so every kernel but EXT runs Fast.
 template <bool HAS_MESH, bool BVH, bool EXT>
 struct MathPolicy {
-  typedef typename std::conditional<!HAS_MESH && !EXT, Fast, Ieee>::type type;
+  typedef typename std::conditional<!EXT, Fast, Ieee>::type type;
 };
 __device__ __forceinline__ V3 ld3(const double* p) { return mk(p[0], p[1], p[2]); }
 
