@@ -1,6 +1,7 @@
 """Time every BASELINE.json config on one MI355X (bench.py covers only the headline C2).
 
     python tools/bench_configs.py [--configs C2,C3,C4,C5] [--spp-scale 1.0] [--cpu]
+    python tools/bench_configs.py --configs E1,E2,E3,E4,E5   # the feature presets (EXT kernels)
 
 One untimed warm-up launch at 1 spp, then one timed frame (HIP events on the launch stream),
 then an instrumented launch (work counters) of the same frame. Prints one JSON line per config.
@@ -26,6 +27,14 @@ CONFIGS = {
     "C3": ("random-scene", 1200, 800, 500, 50),
     "C4": ("bunny", 800, 800, 512, 50),
     "C5": ("david", 1920, 1080, 1024, 50),
+    # not BASELINE configs: the SURVEY 8(f)1 feature presets (EXT kernels: Perlin noise, image
+    # texture, area lights in the dark, a ConstantMedium, MovingSphere) and the list-walk three
+    # spheres, at a common 64 spp, so each has a throughput figure
+    "E1": ("two-perlin-spheres", 800, 450, 64, 50),
+    "E2": ("earth", 800, 450, 64, 50),
+    "E3": ("simple-light", 800, 450, 64, 50),
+    "E4": ("cornell-box-smoke", 800, 800, 64, 50),
+    "E5": ("three-spheres", 800, 450, 64, 50),
 }
 
 

@@ -34,6 +34,7 @@ for s in $STEPS; do
     probe) run ${TAG}_ovf_probe 300 python3 tools/ovf_probe.py ;;
     lanes) run ${TAG}_lane_phases 300 python3 tools/lane_phases.py david 960 540 16 bunny 800 800 16 cornell-box 800 800 16 random-scene 600 400 16 ;;
     bench_s3) run ${TAG}_bench_cornell_s3 600 python3 bench.py --steps 20 --warmup 5 --streams 3 --cpu-spp 0 --david-spp 0 ;;
+    configs_ext) run ${TAG}_bench_configs_ext 600 python3 tools/bench_configs.py --configs E1,E2,E3,E4,E5 ;;
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
