@@ -38,7 +38,7 @@ for s in $STEPS; do
     smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_cornell 600 python3 bench.py --steps 20 --warmup 5 ;;
     prof_cornell) PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
-    prof_cornell_s1) PFX=cornell_s1_ BENCH_ARGS="--steps 3 --warmup 1 --cpu-spp 0 --no-stats --streams 1" PASSES="trace" bash tools/profile.sh || exit 1 ;;
+    prof_cornell_s1) PFX=cornell_s1_ BENCH_ARGS="--steps 3 --warmup 1 --cpu-spp 0 --no-stats --streams 1 --david-spp 0" PASSES="trace" bash tools/profile.sh || exit 1 ;;
     prof_cornell_more) PFX=cornell_ PASSES="stall mem" bash tools/profile.sh || exit 1 ;;
     prof_david) PFX=david_ PROG="tools/render_once.py david 960 540 16 2" PASSES="trace fetch write valu mix" bash tools/profile.sh || exit 1 ;;
     prof_c4) PFX=c4_ PROG="tools/render_once.py bunny 800 800 32 1" PASSES="trace fetch write" bash tools/profile.sh || exit 1 ;;

@@ -8,7 +8,7 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH_ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --cpu-spp 0 --no-stats"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --cpu-spp 0 --no-stats --david-spp 0"}
 # PROG overrides the profiled program (default bench.py), e.g. PROG="tools/render_once.py david 960 540 16"
 PROG=${PROG:-"bench.py $BENCH_ARGS"}
 step() {
