@@ -246,7 +246,7 @@ typedef struct yart_render_stats {
   uint64_t scatter_lanes;       /* lanes scattering at a hit, summed over iterations             */
   uint64_t camera_iters;        /* iterations in which some lane starts a camera ray             */
   uint64_t scatter_iters;       /* iterations in which some lane scatters                        */
-  uint64_t reserved[1];
+  uint64_t parked_walks;        /* mesh walks parked for the next bounce (YART_OPT_MESH_PARK)    */
 } yart_render_stats;
 
 typedef void (*yart_progress_fn)(uint64_t pixels_done, void* user);
@@ -477,7 +477,10 @@ enum {
                                   auto: min(64 GiB, a quarter of the device's memory)               */
   YART_OPT_UNITS_PER_WAVE = 8, /* persistent-wave plan: work units per resident wave; 0 (default) = auto:
                                   64 for list-walk scenes, 192 with a mesh or the world BVH          */
-  YART_OPT_COUNT = 9
+  YART_OPT_MESH_PARK = 9,      /* mesh walks stop once their wave's queue is empty and at most this many
+                                  of its 16 quads still walk, and go on at the next bounce with the
+                                  new rays (one mesh object, depth <= 10); 0 = never; default 8   */
+  YART_OPT_COUNT = 10
 };
 int yart_debug_set_option(int option, int64_t value);
 int yart_debug_get_option(int option, int64_t* value);

@@ -932,7 +932,7 @@ def test_deep_mesh_walks_with_the_references_64_slot_stack(dev, wavefront):
     want = o.render(cam, prm, threads=0)
     np.testing.assert_array_equal(img, want)
     assert (img[O.coverage(24, 24)].sum(axis=-1) != 0).mean() > 0.5
-    # the chunked (persistent-wave) plan too, and the instrumented kernel (fused)
+    # the chunked (persistent-wave) plan too, and the instrumented kernel (on the same plan)
     np.testing.assert_array_equal(s.render(cam, yart.render_params(24, 24, 2, 8, samples_per_unit=1)), want)
     img2, st = s.render_with_stats(cam, prm)
     np.testing.assert_array_equal(img2, want)
@@ -1074,6 +1074,35 @@ def _layer_stack():
         d = b.desc()
         _STACK.append((b, d, O.OracleScene(d)))
     return _STACK[0]
+
+
+@pytest.mark.parametrize("rewalk", [0, 1])
+def test_parked_mesh_walks_are_exact(dev, rewalk):
+    """Parked walks (YART_OPT_MESH_PARK, kernels.hip qbvh_coop PARK): in a one-mesh scene on the
+    persistent plan, a walk whose wave has no new rays left and at most 8 busy quads stops, and its
+    quad picks it up at the next iteration, next to the new rays. The bunny frame parks walks
+    (parked_walks > 0) and renders bitwise the oracle's frame and the frame with parking off; under
+    yart_debug_force_rewalk the re-walks (their stacks in the wave's HBM region while other walks
+    are parked) are exact too."""
+    p = yart.Preset("bunny")
+    W, H, spp = 96, 72, 8
+    cam, prm = p.camera(W, H), yart.render_params(W, H, spp, 50)
+    ref = O.OracleScene(p.desc).render(cam, prm, threads=0)
+    assert dev.yart_debug_force_rewalk(0, rewalk) == 0
+    try:
+        s = yart.DeviceScene(p.desc)
+        img, st = s.render_with_stats(cam, prm)
+        plain = s.render(cam, prm)
+        with yart.option("mesh_park", 0):
+            off, st_off = yart.DeviceScene(p.desc).render_with_stats(cam, prm)
+    finally:
+        assert dev.yart_debug_force_rewalk(0, 0) == 0
+    assert st.parked_walks > 0 and st_off.parked_walks == 0
+    if rewalk:
+        assert st.mesh_rewalks > 0
+    np.testing.assert_array_equal(img, ref)
+    np.testing.assert_array_equal(plain, ref)
+    np.testing.assert_array_equal(off, ref)
 
 
 @pytest.mark.parametrize("walk", ["default", "reference_order", "lane_rewalk"])

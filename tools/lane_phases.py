@@ -1,11 +1,13 @@
 """Where the render kernel's lane-slots go, by phase.
 
-The instrumented kernel (yart_render_with_stats) counts, from ballots, how many of a wave's 64 lanes
+The instrumented kernel (yart_render_with_stats, on the frame's own plan: the persistent waves for
+chunked frames since r06) counts, from ballots, how many of a wave's 64 lanes
 work each time a phase's code runs: the cooperative mesh walk's node branch and leaf branch (and the
 quads idle in each walk's drain), the camera-ray branch and the scatter branch of the render loop.
 Prints one JSON line per frame:
 
     python tools/lane_phases.py david 960 540 16 [cornell-box 800 800 16 ...]
+(library options through YART_OPTIONS, e.g. YART_OPTIONS=mesh_park=0)
 """
 import json
 import sys
@@ -37,7 +39,10 @@ def phases(scene, w, h, spp, depth=50):
             "node_branch_lanes": frac(st.coop_node_lanes, 64 * st.coop_node_rounds),
             "leaf_branch_quad_lanes": frac(st.coop_leaf_quad_lanes, 64 * st.coop_leaf_rounds),
             "leaf_branch_triangle_lanes": frac(st.coop_leaf_lanes, 64 * st.coop_leaf_rounds),
-            "drain_idle_quad_slots": frac(st.coop_idle_slots, 16 * st.coop_rounds)})
+            "drain_idle_quad_slots": frac(st.coop_idle_slots, 16 * st.coop_rounds),
+            "walk_calls": st.coop_walks, "walk_rounds_per_call": frac(st.coop_rounds, st.coop_walks),
+            "mesh_segments_per_call": frac(st.segments, st.coop_walks),
+            "parked_walks": st.parked_walks})
     if st.world_iters:
         r["world_walk_iterations"] = st.world_iters
     return r

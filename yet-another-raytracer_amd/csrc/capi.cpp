@@ -42,7 +42,8 @@ static std::atomic<int64_t> g_opt[YART_OPT_COUNT] = {
     {-1},       // YART_OPT_MESH_WAVEFRONT
     {1 << 20},  // YART_OPT_WF_POOL
     {0},        // YART_OPT_SCRATCH_BYTES (0 = auto: min(64 GiB, device memory / 4))
-    {0}         // YART_OPT_UNITS_PER_WAVE (0 = auto: 64 list walk, 192 mesh / world BVH)
+    {0},        // YART_OPT_UNITS_PER_WAVE (0 = auto: 64 list walk, 192 mesh / world BVH)
+    {8}         // YART_OPT_MESH_PARK (busy quads at which a walk parks; 0 = never)
 };
 int64_t opt(int k) { return k >= 0 && k < YART_OPT_COUNT ? g_opt[k].load(std::memory_order_relaxed) : 0; }
 int hip_fail(hipError_t e, const char* what) {
@@ -375,6 +376,14 @@ static int scene_create(int device, const yart_scene_desc* d, yart_scene** out) 
     if (ds.deep && ds.has_ext)
       return fail(YART_ERR_UNSUPPORTED, "a mesh deeper than depth 10 in a scene with media, moving spheres or "
                                         "noise / image textures");
+    // Parked walks (kernels.hip qbvh_coop PARK): the persistent megakernel of a scene with one mesh
+    // object, no EXT features and a mesh of depth <= 10 (its walk stacks in the LDS)
+    uint32_t mesh_objects = 0;
+    for (uint32_t i = 0; i < d->n_objects; ++i) mesh_objects += d->objects[i].kind == YART_PRIM_MESH;
+    bool small = true;
+    for (uint32_t m = 0; m < d->n_meshes; ++m) small = small && built[m].aux.size() < (1u << 30);
+    const int64_t park = opt(YART_OPT_MESH_PARK);
+    ds.park = (mesh_objects == 1 && !ds.deep && !ds.has_ext && small && park > 0) ? (uint32_t)std::min<int64_t>(park, 16) : 0u;
     const int64_t pool = opt(YART_OPT_WF_POOL);
     if (pool >= 256) s->wf_pool = (uint32_t)(std::min<int64_t>(pool, 1ll << 24) / 256 * 256);
   }
@@ -785,7 +794,8 @@ int wf_pass(yart_scene* s, StreamState* st, const RenderArgs& b, hipStream_t str
 namespace yart_impl {
 
 int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hipStream_t stream, Progress* prog) {
-  Plan pl = stats ? Plan{a.spp ? a.spp : 1, a.spp} : plan(s, a, requested);
+  // stats launches take the frame's own plan (r06; fused before, which measured another kernel)
+  Plan pl = plan(s, a, requested);
   StreamState* st = stream_state(s, stream);
   std::lock_guard<std::mutex> frame_lock(st->frame_mu);
   std::vector<hipEvent_t> ev;
@@ -814,7 +824,8 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     push_frame(s, stream, std::move(ev));
     return YART_OK;
   }
-  if (s->dev.deep) {  // the walk stacks' HBM overflow: one region per wave of the largest launch below
+  if (s->dev.deep || s->dev.park) {  // the walk stacks' HBM overflow (deep meshes; PARK: the re-walk's
+                                     // stacks): one region per wave of the largest launch below
     const uint64_t fused_waves = (uint64_t)a.n_blocks, dyn_waves = (uint64_t)s->cu_count * 16;
     const uint64_t units = (uint64_t)a.n_blocks * ((pl.pass_spp + pl.chunk - 1) / pl.chunk);
     const uint64_t waves = (pl.chunk >= a.spp ? fused_waves : std::min(dyn_waves, units)) + 4;
@@ -1036,8 +1047,8 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   std::unique_ptr<double, decltype(&hipFree)> hold(d_out, &hipFree);
   HIP_TRY(hipMemsetAsync(d_out, 0, bytes, stream), "hipMemset");
   if (stats) {
-    HIP_TRY(hipMalloc(&d_stats, 24 * sizeof(unsigned long long)), "hipMalloc stats");
-    HIP_TRY(hipMemsetAsync(d_stats, 0, 24 * sizeof(unsigned long long), stream), "hipMemset");
+    HIP_TRY(hipMalloc(&d_stats, 25 * sizeof(unsigned long long)), "hipMalloc stats");
+    HIP_TRY(hipMemsetAsync(d_stats, 0, 25 * sizeof(unsigned long long), stream), "hipMemset");
   }
   std::unique_ptr<unsigned long long, decltype(&hipFree)> hold2(d_stats, &hipFree);
   a.out = d_out;
@@ -1056,7 +1067,7 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
   if (int rc = wait_with_progress({done}, {s->device}, {&pr}, pr.pixels, progress, user)) return rc;
   HIP_TRY(hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, stream), "copy output");
   if (stats) {
-    unsigned long long v[24];
+    unsigned long long v[25];
     HIP_TRY(hipMemcpyAsync(v, d_stats, sizeof v, hipMemcpyDeviceToHost, stream), "copy stats");
     HIP_TRY(hipStreamSynchronize(stream), "copy stats");
     std::memset(stats, 0, sizeof *stats);
@@ -1070,6 +1081,7 @@ int render_host(yart_scene* s, const yart_camera* cam, const yart_render_params*
     stats->coop_node_rounds = v[15]; stats->coop_node_lanes = v[16]; stats->coop_leaf_lanes = v[17];
     stats->coop_leaf_quad_lanes = v[18]; stats->iterations = v[19]; stats->camera_lanes = v[20];
     stats->scatter_lanes = v[21]; stats->camera_iters = v[22]; stats->scatter_iters = v[23];
+    stats->parked_walks = v[24];
   }
   HIP_TRY(hipStreamSynchronize(stream), "copy output");
   return ok();

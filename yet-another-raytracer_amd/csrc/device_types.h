@@ -156,6 +156,7 @@ struct DevScene {
   uint32_t n_world_nodes;
   uint32_t n_plane_dirs;
   uint32_t deep;     // a mesh needs more than kStackSlots stack entries: the 64-slot walk (wavefront only)
+  uint32_t park;     // the persistent mesh kernel's walks park at this many busy quads (0: never; kernels.hip PARK)
 };
 
 }  // namespace yart_dev

@@ -693,7 +693,7 @@ __device__ __forceinline__ void triangle_rec(const double* p, const Ray& r, doub
 }
 
 // --------------------------------------------- L4QBVH::hit (qbvh.rs:381-543)
-constexpr int kNumStats = 24;
+constexpr int kNumStats = 25;
 struct Stats { unsigned long long v[kNumStats]; };
 enum { ST_SAMPLES, ST_SEGMENTS, ST_PRIM, ST_NODES, ST_LEAVES, ST_LEAF_TRIS, ST_LIGHT };  // ST_REWALK = 7 .. 13 below
 enum { ST_OVF_PUSHES = 14 };  // deep meshes: walk-stack entries pushed past the LDS slots into the HBM region
@@ -702,7 +702,8 @@ enum { ST_OVF_PUSHES = 14 };  // deep meshes: walk-stack entries pushed past the
 // the leaf branch and the lanes of the quads at a leaf; the loop's iterations and the lanes starting
 // a camera ray or scattering in them (and the iterations where each of those branches runs).
 enum { ST_NODE_ROUNDS = 15, ST_NODE_LANES = 16, ST_LEAF_LANES = 17, ST_LEAF_QUAD_LANES = 18, ST_ITERS = 19,
-       ST_CAMERA_LANES = 20, ST_SCATTER_LANES = 21, ST_CAMERA_ITERS = 22, ST_SCATTER_ITERS = 23 };
+       ST_CAMERA_LANES = 20, ST_SCATTER_LANES = 21, ST_CAMERA_ITERS = 22, ST_SCATTER_ITERS = 23,
+       ST_PARKS = 24 };  // walks parked (qbvh_coop PARK), one per quad and stop
 
 // Ray octant: x >= 0 | y >= 0 << 1 | z >= 0 << 2, the ORDER_TABLE column (qbvh.rs:14-31); a
 // child's push rank for it is 2 bits of its node record (bvh_build.cpp).
@@ -918,8 +919,12 @@ template <int SLOTS> constexpr int wave_lds_words() {
   return (coop_bytes<SLOTS>() / 4 > kStackSlots * 64) ? coop_bytes<SLOTS>() / 4 : kStackSlots * 64;
 }
 // LDS per wave: the per-lane stack (qbvh_t, world BVH) or the cooperative walk, never both at once
-constexpr int kWaveLdsWords = wave_lds_words<kCoopSlots>();
+// The megakernel's also holds the parked walks' queue (a lane per position, u8) and quad words (PARK).
+constexpr int kParkBytes = 64 + 16 * 4;
+constexpr int kWaveLdsWords = wave_lds_words<kCoopSlots>() + kParkBytes / 4;
 constexpr double kF2bMargin = 0x1p-8;
+// PARK: a walk parks only in calls that staged at least this many new rays (the wave is still fed)
+constexpr uint32_t kParkMinRays = 16u;
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
@@ -1071,16 +1076,21 @@ __device__ __forceinline__ bool coop_check(const __attribute__((address_space(1)
   return h > l && t >= l;
 }
 // Inlined: +4 % david, +11 % bunny over a call (the call site spills the caller's state).
-template <bool STATS, int SLOTS = kCoopSlots, bool OVF = false>
+template <bool STATS, int SLOTS = kCoopSlots, bool OVF = false, bool PARK = false>
 __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray& r, double tmin, double tmax_in,
                                        bool& found, double& t_hit, uint32_t& tri, double& u_hit, double& v_hit,
-                                       uint8_t* __restrict__ lds, Stats& st, uint32_t* __restrict__ ovf = nullptr) {
+                                       uint8_t* __restrict__ lds, Stats& st, uint32_t* __restrict__ ovf = nullptr,
+                                       bool resume = false, bool* parked = nullptr, uint32_t park_quads = 0u) {
   found = false;
+  if (PARK) *parked = false;
   if (__ballot(want) == 0) return;
   const uint32_t lane = __lane_id();
   CoopRay* rays = reinterpret_cast<CoopRay*>(lds);
   uint32_t* qstk = reinterpret_cast<uint32_t*>(lds + kCoopRayBytes);
   CoopEnt* qent = reinterpret_cast<CoopEnt*>(lds + kCoopRayBytes + SLOTS * 16 * 4);
+  // PARK: the queue (position -> the lane whose record it is) and the parked quads' words
+  uint8_t* const qtab = lds + coop_bytes<SLOTS>();
+  uint32_t* const qsave = reinterpret_cast<uint32_t*>(lds + coop_bytes<SLOTS>() + 64);
   // The mesh's pointers once, in registers: read through M in the loop, they are reloaded each
   // round (M is a generic pointer the LDS stores might alias) — a dependent memory round trip.
   const gfloat4p nodes = (gfloat4p)M.nodes, leaves = (gfloat4p)M.leaves;
@@ -1090,14 +1100,22 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
   // block, as before the cull: held across the pool's ballot, the constants cost the walk loop
   // registers.
   bool walk = false;
-  if (want) walk = coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in).walk;
+  if (want && !(PARK && resume)) walk = coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in).walk;
   const uint64_t act = __ballot(walk);
-  if (act == 0) return;
+  const uint64_t held = PARK ? __ballot(resume) : 0ull;  // lanes whose parked walk goes on here
+  if (act == 0 && held == 0) return;
   const uint32_t n = (uint32_t)__popcll(act);
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  if (walk) coop_write(rays[rank], r, tmax_in, coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in));
+  if (walk) {
+    // PARK: a lane's record is its own (a parked ray keeps its record across calls), and the queue
+    // lists the new rays' lanes in lane order; otherwise the records are the queue
+    coop_write(rays[PARK ? lane : rank], r, tmax_in, coop_stage(M, aux != nullptr, r, (float)(tmin - fabs(tmin) * 0x1p-20), tmax_in));
+    if (PARK) qtab[rank] = (uint8_t)lane;
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t q = lane >> 2, c = lane & 3u;
+  // the quad's ray: its queue position (< n), or with PARK its record (a lane, kNoRay for none)
+  constexpr uint32_t kNoRay = 64u;
   uint32_t ray = q, next = 16;
   // W's exact check after the walk, per lane (the 32-slot walks only: the per-lane re-walk,
   // qbvh_t, has a 32-slot stack; the 64-slot walks check W where the ray's walk ends)
@@ -1137,10 +1155,77 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     pos = fl >> 1;
     restart((fl & 1u) != 0u);
   };
-  if (ray < n) take();
+  // PARK: a quad that ran out of rays while few others still walk does not wait for them. The walk
+  // stops and the busy quads park: the next node goes back on the quad's stack (entry 0, never
+  // dropped), the best hit's leaf, key and found flag into the ray's record (its t, u, v are there
+  // already), the stack depth and the ray into the quad's word. The lane renders on with its other
+  // lanes and calls again with `resume`; the same quad picks the walk up where it stopped. Every
+  // value the walk carries is restored as it was (the f32 constants are formed again from the
+  // record, as at staging), so each quad takes the same steps in the same order: the same answer.
+  auto park = [&]() {
+    if (STATS && c == 0u) st.v[ST_PARKS]++;
+    if (c == 0u) {
+      const int slot = cursor * 16 + (int)q;
+      qstk[slot] = node;
+      qent[slot] = (CoopEnt)0;
+      CoopRay& s = rays[ray];
+      s.flags = 0x40000000u | bleaf;  // bits 31-30 = 01: parked (a finished walk writes 1x or 00)
+      s.inv32[1] = __uint_as_float(fnd ? 1u : 0u);
+      s.inv32[2] = __uint_as_float(bkey);
+      qsave[q] = 0x80000000u | (ray << 8) | (uint32_t)(cursor + 1);
+    }
+  };
+  auto unpark = [&](uint32_t depth) {
+    const CoopRay& s = rays[ray];
+    Ray wr;
+    wr.o = mk(s.o[0], s.o[1], s.o[2]);
+    wr.d = mk(s.d[0], s.d[1], s.d[2]);
+    wr.time = 0.0; wr.wl = 0.0;
+    const double tin = s.tmax;
+    const CoopStage g = coop_stage(M, aux != nullptr, wr, tmin32, tin);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      inv32[j] = g.inv32[j];
+      c32[j] = vfloat2{g.c32[2 * j], g.c32[2 * j + 1]};
+    }
+    pos = g.flags >> 1;
+    f2b = (g.flags & 1u) != 0u;
+    bleaf = s.flags & 0x3FFFFFFFu;
+    fnd = __float_as_uint(s.inv32[1]) != 0u;
+    bkey = __float_as_uint(s.inv32[2]);
+    tb = fnd ? coop_get_d(&s.c32[0]) : tin;
+    if (f2b && fnd) {  // as the leaf step set them at the best hit
+      const double lim = tb * (1.0 + kF2bMargin);
+      const double teff = lim < tin ? lim : tin;
+      teff32 = (float)(teff + teff * 0x1p-20);
+      bound = (float)lim;
+    } else {  // as restart() set them
+      teff32 = (float)(tin + fabs(tin) * 0x1p-20);
+      bound = INFINITY;
+    }
+    cursor = (int)depth - 1;
+    node = qstk[cursor * 16 + (int)q];
+  };
+  if (PARK) {  // parked quads first, on their own rays; the others take the queue's
+    const uint32_t sv = held ? qsave[q] : 0u;
+    const bool res = (sv >> 31) != 0u;
+    const uint64_t fm0 = __ballot(!res && c == 0u);
+    const uint32_t idx = (uint32_t)__popcll(fm0 & ((1ull << (4u * q)) - 1ull));
+    next = (uint32_t)__popcll(fm0);
+    if (res) {
+      ray = (sv >> 8) & 63u;
+      unpark(sv & 0xFFu);
+      if (c == 0u) qsave[q] = 0u;
+    } else {
+      ray = idx < n ? (uint32_t)qtab[idx] : kNoRay;
+      if (ray != kNoRay) take();
+    }
+  } else if (ray < n) {
+    take();
+  }
   if (STATS && lane == 0) st.v[ST_WALKS]++;
   for (;;) {
-    const bool has = ray < n;
+    const bool has = PARK ? ray != kNoRay : ray < n;
     if (__ballot(has) == 0) break;
     if (STATS) {  // the ballots outside the lane-0 branch: they must see every quad
       const uint64_t at_node = __ballot(has && !(node >> 31));
@@ -1331,10 +1416,25 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
     const uint64_t fm = __ballot(fin && c == 0);
     if (fm) {
       if (fin) {
-        ray = next + (uint32_t)__popcll(fm & ((1ull << (4u * q)) - 1ull));
-        if (ray < n) take();
+        const uint32_t idx = next + (uint32_t)__popcll(fm & ((1ull << (4u * q)) - 1ull));
+        if (PARK) {
+          ray = idx < n ? (uint32_t)qtab[idx] : kNoRay;
+          if (ray != kNoRay) take();
+        } else {
+          ray = idx;
+          if (ray < n) take();
+        }
       }
       next += (uint32_t)__popcll(fm);
+    }
+    // PARK: the queue is empty and at most park_quads quads still walk (a call that staged at least
+    // kParkMinRays new rays: with fewer, the lanes are running out of work and the walks finish here)
+    if (PARK && park_quads != 0u && n >= kParkMinRays && next >= n) {
+      const bool busy = ray != kNoRay;
+      if ((uint32_t)__popcll(__ballot(busy && c == 0u)) <= park_quads) {
+        if (busy) park();
+        break;
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1345,23 +1445,30 @@ __device__ __forceinline__ void qbvh_coop(const DevMesh& M, bool want, const Ray
   // wave's LDS, free once every lane has read its record) — rare.
   bool redo = false;
   Ray wr;  // the walked ray, read back from its record (the caller's copy need not live through the walk)
-  if (walk) {
-    const CoopRay& s = rays[rank];
-    found = __float_as_uint(s.inv32[1]) != 0u;
-    t_hit = coop_get_d(&s.c32[0]); u_hit = coop_get_d(&s.c32[2]); v_hit = coop_get_d(&s.c32[4]);
-    tri = __float_as_uint(s.inv32[0]);
+  if (walk || (PARK && resume)) {
+    const CoopRay& s = rays[PARK ? lane : rank];
     const uint32_t fl = s.flags;
-    if (kPostCheck && (fl >> 31)) {
-      wr.o = mk(s.o[0], s.o[1], s.o[2]);
-      wr.d = mk(s.d[0], s.d[1], s.d[2]);
-      redo = !coop_check(aux, fl & 0x3FFFFFFFu, wr, tmin, tmax_in, t_hit) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+    if (PARK && (fl >> 30) == 1u) {
+      *parked = true;  // its walk goes on at the next call
+    } else {
+      found = __float_as_uint(s.inv32[1]) != 0u;
+      t_hit = coop_get_d(&s.c32[0]); u_hit = coop_get_d(&s.c32[2]); v_hit = coop_get_d(&s.c32[4]);
+      tri = __float_as_uint(s.inv32[0]);
+      if (kPostCheck && (fl >> 31)) {
+        wr.o = mk(s.o[0], s.o[1], s.o[2]);
+        wr.d = mk(s.d[0], s.d[1], s.d[2]);
+        redo = !coop_check(aux, fl & 0x3FFFFFFFu, wr, tmin, tmax_in, t_hit) || __builtin_amdgcn_readfirstlane(g_force_rewalk) != 0u;
+      }
     }
   }
   if (kPostCheck && __ballot(redo) != 0ull) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (redo) {
       if (STATS) st.v[ST_REWALK]++;
-      found = qbvh_t<STATS, OVF>(M, wr, tmin, tmax_in, t_hit, tri, u_hit, v_hit, reinterpret_cast<uint32_t*>(lds) + lane, st, ovf);
+      // PARK: parked walks keep their records and stacks in the LDS; the re-walk's stack is this
+      // lane's column of the wave's HBM region instead
+      uint32_t* const rstk = (PARK && park_quads) ? ovf + 2 * kOvfQuadWords + lane : reinterpret_cast<uint32_t*>(lds) + lane;
+      found = qbvh_t<STATS, OVF>(M, wr, tmin, tmax_in, t_hit, tri, u_hit, v_hit, rstk, st, ovf);
     }
   }
 }
@@ -1481,11 +1588,12 @@ __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
   return *(const T*)((cptr)base + __builtin_amdgcn_readfirstlane(i));
 }
 
-template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false>
+template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false, bool PARK = false>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                              uint32_t* ovf = nullptr) {
+                                              uint32_t* ovf = nullptr, bool resume = false, bool* parked = nullptr) {
   bool found = false;
+  if (PARK) *parked = false;
   double closest = tmax;
   uint32_t who = 0;  // obj << 3 | sub (the kernels without meshes)
   id.u = 0.0; id.v = 0.0; id.obj = 0; id.sub = 0;
@@ -1498,7 +1606,8 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       bool hit;
       double t, u, v;
       uint32_t sub;
-      qbvh_coop<STATS, SLOTS, OVF>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st, ovf);
+      qbvh_coop<STATS, SLOTS, OVF, PARK>(uniform_at(S.meshes, o.mesh), want, lr, tmin, closest, hit, t, sub, u, v, coop, st, ovf,
+                                         resume, parked, S.park);
       if (hit) {
         closest = t;
         id.obj = i; id.sub = sub; id.u = u; id.v = v;
@@ -1764,15 +1873,17 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   return found;
 }
 
-template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false>
+template <bool HAS_MESH, bool BVH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false, bool PARK = false>
 __device__ __forceinline__ bool world_hit(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, Hit& rec,
                                           int32_t& which, uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
-                                          uint32_t* ovf = nullptr) {
+                                          uint32_t* ovf = nullptr, bool resume = false, bool* parked = nullptr) {
   HitId id;
   if constexpr (BVH) {  // no media or meshes in BVH scenes (capi.cpp)
     if (!world_closest_bvh<STATS>(S, r, tmin, tmax, id, stk, st)) return false;
   } else {
-    if (!world_closest<HAS_MESH, STATS, EXT, SLOTS, OVF>(S, want, r, tmin, tmax, id, stk, coop, st, q, ovf) || !want) return false;
+    if (!world_closest<HAS_MESH, STATS, EXT, SLOTS, OVF, PARK>(S, want, r, tmin, tmax, id, stk, coop, st, q, ovf, resume, parked) ||
+        !want || (PARK && *parked))
+      return false;
   }
   hit_record<HAS_MESH, EXT>(S, r, id, rec);
   which = (int32_t)id.obj;
@@ -2207,6 +2318,10 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
   // The mesh kernel's LDS is nearly full (36.9 KB of walk state per workgroup): it keeps three
   // words (pixel, sample, block) and derives x, y and the slot from the pixel where needed.
   constexpr bool JOBL = DYN && !HAS_MESH, JOBL3 = DYN && HAS_MESH;
+  // PARK (qbvh_coop): the persistent mesh kernel lets a walk whose wave ran out of rays stop and go on
+  // at the next iteration, with the rays the other lanes bring; S.park (the busy-quad threshold, 0 =
+  // off) is set for scenes with one mesh object.
+  constexpr bool PARK = HAS_MESH && DYN && !EXT && !DEEP;
   __shared__ uint32_t s_job[JOBL ? 4 * 6 * 64 : JOBL3 ? 4 * 3 * 64 : 1];
   // the wave index through readfirstlane: uniform, so the per-wave LDS bases live in SGPRs (as a
   // VGPR the mesh walk's stack base was spilled and reloaded at every pop)
@@ -2231,7 +2346,11 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
   uint32_t* stk = &s_stack[HAS_MESH ? (wave * kWaveLdsWords + lane) : BVH ? (wave * kStackSlots * 64 + lane) : 0];
   uint8_t* coop = reinterpret_cast<uint8_t*>(&s_stack[HAS_MESH ? wave * kWaveLdsWords : 0]);
   // DEEP: this wave's HBM stack region (one per resident wave: the grid's waves, capi.cpp launch_frame)
-  uint32_t* const ovf = DEEP ? A.stack_ovf + (size_t)(blockIdx.x * 4u + wave) * kOvfWords : nullptr;
+  uint32_t* const ovf = (DEEP || PARK) ? A.stack_ovf + (size_t)(blockIdx.x * 4u + wave) * kOvfWords : nullptr;
+  if (PARK) {  // no parked quads yet
+    if (lane < 16u) reinterpret_cast<uint32_t*>(coop + coop_bytes<kCoopSlots>() + 64)[lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
   Stats st;
   if (STATS) for (int i = 0; i < kNumStats; ++i) st.v[i] = 0;
 
@@ -2247,6 +2366,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
   uint64_t cov = 0;                   // DYN: the unit's block slots that are rendered (wave-uniform)
   bool drained = false;               // DYN: the queue has no units left (wave-uniform)
   bool need = true;                   // DYN: this lane wants a job
+  bool parked = false;                // PARK: this lane's mesh walk stopped; the same ray again
   bool alive = DYN ? true : (active && smp < s_stop);
   Rng g;
   Ray ray;
@@ -2341,7 +2461,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
     if (__ballot(run) == 0) break;
     // T is the path's throughput while it runs and its result R (ray_reflectance's return value)
     // once it has ended (term): one register pair for both, since no lane needs both at once.
-    bool term = false, want = false;
+    bool term = false, want = PARK && parked;  // a parked lane's ray, T and depth are as they were
     if (STATS) {
       const uint64_t cam = __ballot(run && fresh), sca = __ballot(run && !fresh);
       if (lane == 0) {
@@ -2352,7 +2472,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
         st.v[ST_SCATTER_ITERS] += sca ? 1u : 0u;
       }
     }
-    if (run) {
+    if (run && !(PARK && parked)) {
       // One Philox site per iteration for every lane: blocks 0-1 of this iteration's phase, the
       // camera ray of a fresh sample (phase 0) or the scatter of the hit the previous iteration
       // found (phase max_depth - depth + 1, its bounce level).
@@ -2410,7 +2530,13 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
       bool scat = false;
       const QueryCtx q{g.k0, g.k1, JL ? jl[64] : smp, JL ? jl[0] : pixel, A.max_depth - depth + 1u};
       if (HAS_MESH) {  // converged: every lane, `want` says which have a ray
-        hit = world_hit<HAS_MESH, BVH, STATS, EXT, kCoopSlots, DEEP>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q, ovf);
+        bool now = false;
+        hit = world_hit<HAS_MESH, BVH, STATS, EXT, kCoopSlots, DEEP, PARK>(S, want, ray, 0.001, INFINITY, h, which, stk, coop, st, q,
+                                                                          ovf, parked, &now);
+        if (PARK) {
+          parked = now;
+          want = want && !now;  // its hit is not known yet: nothing more for this lane in this iteration
+        }
       } else if (want) {
         hit = world_hit<HAS_MESH, BVH, STATS, EXT>(S, true, ray, 0.001, INFINITY, h, which, stk, coop, st, q);
       }
@@ -2876,22 +3002,25 @@ hipError_t launch_accumulate(const RenderArgs& a, bool first_pass, hipStream_t s
   return hipGetLastError();
 }
 hipError_t launch_render(const DevScene& s, const RenderArgs& a, bool stats, hipStream_t stream) {
-  const bool dyn = a.scratch != nullptr;  // stats launches are always fused (see capi.cpp)
+  const bool dyn = a.scratch != nullptr;  // stats launches follow the same plan (r06: they were fused)
   const uint32_t units = a.n_blocks * a.n_chunks;
   const uint32_t grid = ((dyn && a.waves < units ? a.waves : units) + 3) / 4;
   if (grid == 0) return hipSuccess;
 #define YART_LAUNCH(MESH, BVH, EXT)                                                                            \
   do {                                                                                                        \
-    if (stats) hipLaunchKernelGGL((k_render<MESH, BVH, true, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);  \
+    if (stats && dyn) hipLaunchKernelGGL((k_render<MESH, BVH, true, true, EXT>), dim3(grid), dim3(256), 0, stream, s, a); \
+    else if (stats) hipLaunchKernelGGL((k_render<MESH, BVH, true, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);  \
     else if (dyn) hipLaunchKernelGGL((k_render<MESH, BVH, false, true, EXT>), dim3(grid), dim3(256), 0, stream, s, a); \
     else hipLaunchKernelGGL((k_render<MESH, BVH, false, false, EXT>), dim3(grid), dim3(256), 0, stream, s, a);        \
   } while (0)
   if (s.has_mesh && s.deep && !s.has_ext) {  // deep meshes: stacks overflow into a.stack_ovf (capi.cpp)
     if (!a.stack_ovf) return hipErrorInvalidValue;
-    if (stats) hipLaunchKernelGGL((k_render<true, false, true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    if (stats && dyn) hipLaunchKernelGGL((k_render<true, false, true, true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
+    else if (stats) hipLaunchKernelGGL((k_render<true, false, true, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
     else if (dyn) hipLaunchKernelGGL((k_render<true, false, false, true, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
     else hipLaunchKernelGGL((k_render<true, false, false, false, false, true>), dim3(grid), dim3(256), 0, stream, s, a);
   } else if (s.has_mesh) {
+    if (s.park && dyn && !a.stack_ovf) return hipErrorInvalidValue;  // PARK: the re-walk's HBM stacks
     if (s.has_ext) YART_LAUNCH(true, false, true); else YART_LAUNCH(true, false, false);
   } else if (s.world_nodes) {
     if (s.has_ext) YART_LAUNCH(false, true, true); else YART_LAUNCH(false, true, false);  // noise textures only

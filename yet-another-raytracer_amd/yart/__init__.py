@@ -150,7 +150,8 @@ def load_device():
 
 # yart_debug_set_option keys (include/yart.h YART_OPT_*)
 OPTIONS = {"qbvh_ties_desc": 0, "qbvh_threads": 1, "walk_tree": 2, "mesh_walk_ref": 3, "world_bvh": 4,
-           "mesh_wavefront": 5, "wf_pool": 6, "scratch_bytes": 7, "units_per_wave": 8}
+           "mesh_wavefront": 5, "wf_pool": 6, "scratch_bytes": 7, "units_per_wave": 8,
+           "mesh_park": 9}
 
 
 def get_option(name):

@@ -95,7 +95,7 @@ class RenderStats(C.Structure):
                 ("coop_node_rounds", C.c_uint64), ("coop_node_lanes", C.c_uint64), ("coop_leaf_lanes", C.c_uint64),
                 ("coop_leaf_quad_lanes", C.c_uint64), ("iterations", C.c_uint64), ("camera_lanes", C.c_uint64),
                 ("scatter_lanes", C.c_uint64), ("camera_iters", C.c_uint64), ("scatter_iters", C.c_uint64),
-                ("reserved", C.c_uint64 * 1)]
+                ("parked_walks", C.c_uint64)]
 
 
 class RenderDefaults(C.Structure):
