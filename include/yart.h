@@ -474,7 +474,8 @@ enum {
                                   without media / moving spheres / noise or image textures */
   YART_OPT_WF_POOL = 6,        /* wavefront path slots, >= 256 (rounded down to a multiple of 256), default 2^20 */
   YART_OPT_SCRATCH_BYTES = 7,  /* sample-scratch budget per pass and stream in bytes; 0 (default) =
-                                  auto: min(64 GiB, a quarter of the device's memory)               */
+                                  auto: min(16 GiB, an eighth of the device's memory); a frame
+                                  that needs more renders in overlapped passes over two halves  */
   YART_OPT_UNITS_PER_WAVE = 8, /* persistent-wave plan: work units per resident wave; 0 (default) = auto:
                                   64 for list-walk scenes, 192 with a mesh or the world BVH          */
   YART_OPT_MESH_PARK = 9,      /* mesh walks stop once their wave's queue is empty and at most this many

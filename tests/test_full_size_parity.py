@@ -68,19 +68,23 @@ def test_config_full_frame_bitwise(cfg, scene, W, H, spp, depth, stride):
 
 
 def test_c5_in_one_pass_and_in_scratch_passes_agree():
-    """C5's sample scratch is 49.8 MB per sample, 51 GB for the frame: the auto budget (min(64 GiB,
-    device memory / 4), capi.cpp scratch_budget) renders it in ONE pass on an MI355X, the old
-    4 GiB budget in 12 passes, each with its own accumulate. The two plans must give the same
+    """C5's sample scratch is 49.8 MB per sample, 51 GB for the frame: the auto budget (min(16 GiB,
+    device memory / 8), capi.cpp scratch_budget) renders it in 7 overlapped passes over two 8 GiB
+    halves (r06), a 4 GiB budget in 25 over two 2 GiB halves, a 64 GiB budget in ONE pass; each pass
+    with its own accumulate, the odd ones rendered on a helper stream. The plans must give the same
     frame bit for bit (k_accumulate adds samples in sample order whatever the split), so the
-    oracle check of test_config_full_frame_bitwise[C5] covers both."""
+    oracle check of test_config_full_frame_bitwise[C5] (the auto plan) covers them all."""
     W, H, spp, depth = 1920, 1080, 1024, 50
     per_sample = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 3 * 8
     assert yart.get_option("scratch_bytes") == 0  # auto
-    assert per_sample * spp <= 64 << 30 and (4 << 30) // per_sample < spp
+    assert per_sample * spp <= 64 << 30 and (16 << 30) // per_sample < spp
     p = yart.Preset("david")
     cam = p.camera(W, H)
     s = yart.DeviceScene(p)
-    one = s.render(cam, yart.render_params(W, H, spp, depth))
+    auto = s.render(cam, yart.render_params(W, H, spp, depth))
+    with yart.option("scratch_bytes", 64 << 30):
+        one = s.render(cam, yart.render_params(W, H, spp, depth))
     with yart.option("scratch_bytes", 4 << 30):
         split = s.render(cam, yart.render_params(W, H, spp, depth))
+    assert np.array_equal(one, auto)
     assert np.array_equal(one, split)

@@ -716,8 +716,32 @@ def test_chunked_multi_pass_and_shards(dev, opt):
     np.testing.assert_array_equal(parts[0] + parts[1], ref)
 
 
+def test_overlapped_scratch_passes_back_to_back(dev, opt):
+    """A frame larger than the scratch budget renders in overlapped passes (capi.cpp launch_frame):
+    the odd passes render on a helper stream into the scratch's second half and the accumulates run
+    in pass order on another. Frames enqueued back to back on one stream, with halves of 1, 2 and 3
+    samples (several passes each, the mesh frame's overflow regions doubled too) and one frame in a
+    single pass between them, must equal their one-pass renders bit for bit."""
+    import torch
+    st = torch.cuda.current_stream()
+    for scene, W, H, spps in [("cornell-box", 48, 40, [7, 5, 9, 6, 4]), ("bunny", 40, 32, [5, 4, 7])]:
+        p = yart.Preset(scene)
+        cam = p.camera(W, H)
+        s = yart.DeviceScene(p)
+        per = ((W + 7) // 8) * ((H + 7) // 8) * 64 * 24
+        refs = [s.render(cam, yart.render_params(W, H, n, 50)) for n in spps]
+        outs = [torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0") for _ in spps]
+        for k, (n, out) in enumerate(zip(spps, outs)):
+            opt("scratch_bytes", per * 64 if k == 3 else per * 2 * (k % 3 + 1))
+            s.render_async(cam, yart.render_params(W, H, n, 50, samples_per_unit=1), out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        for k, (out, ref) in enumerate(zip(outs, refs)):
+            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"{scene} frame {k}")
+    assert (refs[0][O.coverage(W, H)].sum(axis=-1) != 0).mean() > 0.05
+
+
 def test_scratch_pass_shrinks_when_the_device_is_nearly_full(dev):
-    """The auto scratch budget (min(64 GiB, device memory / 4), capi.cpp scratch_budget) is sized
+    """The auto scratch budget (min(16 GiB, device memory / 8), capi.cpp scratch_budget) is sized
     from the device's total memory, not what is free. With all but ~1.5 GB of the device held by
     another allocation, a 1920x1080x64 frame (3.2 GB of sample scratch in one pass) cannot get
     its pass: pass_scratch halves it until the allocation fits (64 -> 32 -> 16 samples), and the

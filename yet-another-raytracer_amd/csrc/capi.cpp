@@ -41,7 +41,7 @@ static std::atomic<int64_t> g_opt[YART_OPT_COUNT] = {
     {-1},       // YART_OPT_WORLD_BVH
     {-1},       // YART_OPT_MESH_WAVEFRONT
     {1 << 20},  // YART_OPT_WF_POOL
-    {0},        // YART_OPT_SCRATCH_BYTES (0 = auto: min(64 GiB, device memory / 4))
+    {0},        // YART_OPT_SCRATCH_BYTES (0 = auto: min(16 GiB, device memory / 8))
     {0},        // YART_OPT_UNITS_PER_WAVE (0 = auto: 64 list walk, 192 mesh / world BVH)
     {8}         // YART_OPT_MESH_PARK (busy quads at which a walk parks; 0 = never)
 };
@@ -148,6 +148,11 @@ yart_scene::~yart_scene() {
     if (kv.second->wf_mem) (void)hipFree(kv.second->wf_mem);
     if (kv.second->ovf) (void)hipFree(kv.second->ovf);
     if (kv.second->wf_status_host) (void)hipHostFree(kv.second->wf_status_host);
+    StreamState& t = *kv.second;
+    for (hipStream_t x : {t.aux, t.acc})
+      if (x) (void)hipStreamDestroy(x);
+    for (hipEvent_t e : {t.ev_start, t.ev_render[0], t.ev_render[1], t.ev_acc[0], t.ev_acc[1]})
+      if (e) (void)hipEventDestroy(e);
   }
   for (hipStream_t st : owned_streams) (void)hipStreamDestroy(st);
   for (auto& kv : frames)
@@ -550,22 +555,29 @@ namespace {
 // When the shard has too few blocks to fill the device several times over (strong scaling, small
 // frames) the samples are split into chunks; each sample's value then goes to HBM and
 // k_accumulate adds them per pixel in sample order, so the sums do not depend on the split.
-struct Plan { uint32_t chunk, pass_spp; };
+struct Plan { uint32_t chunk, pass_spp; bool overlap = false; };  // overlap: passes in two scratch halves (launch_frame)
 
-// Sample-scratch bytes one pass may use on a stream. Auto (option 0): a quarter of the device's
-// memory, at most 64 GiB — C5 (david 1920x1080x1024, 49.8 MB per sample) then runs in one pass on
-// an MI355X instead of 12 passes at the old 4 GiB, each of which drained the persistent waves
-// (279.7 -> 319.9 Msamples/s at full spp, profiles/r05j_c5_scratch_sweep.log). Two streams in
-// flight hold at most half the device.
+// Sample-scratch bytes a frame may use on a stream. Auto (option 0): an eighth of the device's
+// memory, at most 16 GiB. C1-C4 and a C5 shard fit in one pass; C5 on one GPU (david
+// 1920x1080x1024, 49.8 MB per sample, 51 GB) renders in 7 overlapped passes over two 8 GiB halves
+// at -0.3 % against one 51 GB pass (r06, profiles/r06r_ab_scratch_overlap2.log; r05 had raised the
+// cap to 64 GiB when passes still ran one after another: 12 passes at 4 GiB cost 13 %).
 uint64_t scratch_budget(const yart_scene* s) {
   const int64_t v = opt(YART_OPT_SCRATCH_BYTES);
   if (v > 0) return (uint64_t)v;
-  const uint64_t cap = 64ull << 30;
-  return s->mem_total ? std::min<uint64_t>(cap, s->mem_total / 4) : (4ull << 30);
+  const uint64_t cap = 16ull << 30;
+  return s->mem_total ? std::min<uint64_t>(cap, s->mem_total / 8) : (4ull << 30);
 }
 Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
   const uint32_t spp = a.spp;
   if (spp == 0 || a.n_blocks == 0) return {spp ? spp : 1, spp};
+  const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
+  const uint64_t budget = scratch_budget(s);
+  // A frame whose samples do not fit the budget renders in passes over two halves of it (overlapped,
+  // launch_frame); the chunks are then cut for a pass, not the frame, so each pass holds as many
+  // units per wave as a one-pass frame (the frame's chunks left 4 units per wave in a C5 pass).
+  const bool split = (uint64_t)spp * per_sample > budget;
+  const uint32_t span = split ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, budget / 2 / per_sample)) : spp;
   uint32_t chunk;
   if (requested) {
     if (requested >= spp) return {spp, spp};  // explicit one-unit-per-block: the fused kernel
@@ -583,18 +595,18 @@ Plan plan(const yart_scene* s, const RenderArgs& a, uint32_t requested) {
     if (upw <= 0) upw = heavy ? 192 : 64;
     const uint64_t target = (uint64_t)upw * (uint64_t)s->cu_count * 16ull;
     uint64_t chunks = (target + a.n_blocks - 1) / a.n_blocks;
-    const uint32_t min_chunk = heavy && spp >= 2 ? 2 : 1;
-    const uint64_t max_chunks = (spp + min_chunk - 1) / min_chunk;  // 31 spp: 16 units of <= 2
+    const uint32_t min_chunk = heavy && span >= 2 ? 2 : 1;
+    const uint64_t max_chunks = (span + min_chunk - 1) / min_chunk;  // 31 spp: 16 units of <= 2
     if (chunks > max_chunks) chunks = max_chunks;
-    chunk = (uint32_t)((spp + chunks - 1) / chunks);
+    chunk = (uint32_t)((span + chunks - 1) / chunks);
   }
-  const uint64_t per_sample = (uint64_t)a.n_blocks * 64 * 3 * sizeof(double);
-  const uint64_t budget = scratch_budget(s);
-  uint64_t pass = budget / per_sample;
+  uint64_t pass = split ? span : budget / per_sample;
   pass = pass / chunk * chunk;
   if (pass < chunk) pass = chunk;
   if (pass > spp) pass = spp;
-  return {chunk, (uint32_t)pass};
+  Plan pl{chunk, (uint32_t)pass};
+  pl.overlap = chunk < spp && pass < spp;
+  return pl;
 }
 
 StreamState* stream_state(yart_scene* s, hipStream_t stream) {
@@ -609,6 +621,8 @@ int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out
   if (st->ovf_bytes < bytes) {
     if (st->ovf) {
       HIP_TRY(hipStreamSynchronize(stream), "drain the stream before growing its stack overflow");
+      for (hipStream_t x : {st->aux, st->acc})
+        if (x) HIP_TRY(hipStreamSynchronize(x), "drain the stream before growing its stack overflow");
       HIP_TRY(hipFree(st->ovf), "hipFree stack overflow");
     }
     st->ovf = nullptr; st->ovf_bytes = 0;
@@ -629,16 +643,20 @@ int stream_ovf(StreamState* st, hipStream_t stream, size_t bytes, uint32_t** out
 // buffer is allocated BEFORE the working one is released: on a nearly full device a frame then
 // costs a failed hipMalloc or two and runs in the buffer it has, with no stream drain and no
 // free/re-allocate churn per frame, and grows as soon as the memory is there.
+// halves = 2: two such buffers back to back (the overlapped passes of launch_frame).
 int pass_scratch(StreamState* st, hipStream_t stream, const RenderArgs& a, Plan& pl, uint32_t min_spp,
-                 double** out) {
+                 double** out, uint32_t halves = 1) {
   for (;;) {
-    const size_t bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double) + 256;
+    const size_t bytes = halves * ((size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double) + 256);
     if (st->bytes >= bytes) { *out = st->scratch; return YART_OK; }
     double* grown = nullptr;
     const hipError_t e = hipMalloc(&grown, bytes);
     if (e == hipSuccess) {
       if (st->scratch) {
-        const hipError_t d = hipStreamSynchronize(stream);  // earlier frames may still use the old one
+        // earlier frames may still use the old one (their overlapped passes too)
+        hipError_t d = hipStreamSynchronize(stream);
+        for (hipStream_t x : {st->aux, st->acc})
+          if (x && d == hipSuccess) d = hipStreamSynchronize(x);
         if (d != hipSuccess) { (void)hipFree(grown); return hip_fail(d, "drain the stream before growing its scratch"); }
         HIP_TRY(hipFree(st->scratch), "hipFree scratch");
       }
@@ -824,12 +842,22 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     push_frame(s, stream, std::move(ev));
     return YART_OK;
   }
+  // A frame larger than the scratch budget renders in passes, and the passes overlap (r06): the
+  // budget is split in two halves, the odd passes render on the stream's `aux` stream into the second
+  // half while the previous pass's last waves finish, and k_accumulate adds the passes in pass order
+  // on `acc`; a half is rendered into again once the accumulate two passes back has read it. The sums
+  // are the same (the accumulates run in order); the frame starts and ends in the caller's stream
+  // order. (One pass after another, each pass's tail idled the device: C5 on 16 GiB, 4 passes,
+  // -3 %; 8 GiB, 7 passes, -5.6 %; profiles/r06r_ab_scratch_budget.log.)
+  bool overlap = pl.overlap;
+  uint64_t ovf_words = 0;  // one launch's overflow region (a second one for the overlapped passes)
   if (s->dev.deep || s->dev.park) {  // the walk stacks' HBM overflow (deep meshes; PARK: the re-walk's
                                      // stacks): one region per wave of the largest launch below
     const uint64_t fused_waves = (uint64_t)a.n_blocks, dyn_waves = (uint64_t)s->cu_count * 16;
     const uint64_t units = (uint64_t)a.n_blocks * ((pl.pass_spp + pl.chunk - 1) / pl.chunk);
     const uint64_t waves = (pl.chunk >= a.spp ? fused_waves : std::min(dyn_waves, units)) + 4;
-    if (int rc = stream_ovf(st, stream, waves * kOvfWords * sizeof(uint32_t), &a.stack_ovf)) return rc;
+    ovf_words = waves * kOvfWords;
+    if (int rc = stream_ovf(st, stream, (overlap ? 2 : 1) * ovf_words * sizeof(uint32_t), &a.stack_ovf)) return rc;
   }
   if (pl.chunk >= a.spp) {  // fused: one unit per block, sums in registers
     if (prog) prog->total_units = a.n_blocks;
@@ -841,32 +869,66 @@ int launch_frame(yart_scene* s, RenderArgs a, uint32_t requested, bool stats, hi
     return YART_OK;
   }
   double* scratch = nullptr;
-  if (int rc = pass_scratch(st, stream, a, pl, pl.chunk, &scratch)) return rc;
-  const size_t scratch_bytes = (size_t)a.n_blocks * pl.pass_spp * 64 * 3 * sizeof(double);
-  uint32_t* queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scratch) + scratch_bytes);
+  if (int rc = pass_scratch(st, stream, a, pl, pl.chunk, &scratch, overlap ? 2u : 1u)) return rc;
+  overlap = overlap && pl.pass_spp < a.spp;
+  if (overlap && !st->acc) {  // the stream's first overlapped frame: its two helper streams and events
+    DeviceGuard g(s->device);
+    hipStream_t x[2] = {nullptr, nullptr};
+    hipEvent_t e[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipError_t err = hipSuccess;
+    for (int i = 0; i < 2 && err == hipSuccess; ++i) err = hipStreamCreateWithFlags(&x[i], hipStreamNonBlocking);
+    for (int i = 0; i < 5 && err == hipSuccess; ++i) err = hipEventCreateWithFlags(&e[i], hipEventDisableTiming);
+    if (err != hipSuccess) {
+      for (hipStream_t y : x) if (y) (void)hipStreamDestroy(y);
+      for (hipEvent_t y : e) if (y) (void)hipEventDestroy(y);
+      return hip_fail(err, "create the overlapped passes' streams");
+    }
+    st->aux = x[0]; st->acc = x[1];
+    st->ev_start = e[0]; st->ev_render[0] = e[1]; st->ev_render[1] = e[2]; st->ev_acc[0] = e[3]; st->ev_acc[1] = e[4];
+  }
+  const size_t half_doubles = (size_t)a.n_blocks * pl.pass_spp * 64 * 3;
+  const size_t half_bytes = half_doubles * sizeof(double) + 256;
   const uint32_t passes = (a.spp + pl.pass_spp - 1) / pl.pass_spp;
   if (int rc = take_events(s, 3 * (size_t)passes, ev)) return rc;
+  if (overlap) {  // the helper streams start after the caller's earlier work
+    HIP_TRY(hipEventRecord(st->ev_start, stream), "hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(st->aux, st->ev_start, 0), "hipStreamWaitEvent");
+    HIP_TRY(hipStreamWaitEvent(st->acc, st->ev_start, 0), "hipStreamWaitEvent");
+  }
   uint32_t k = 0, base = 0;
   for (uint32_t s0 = 0; s0 < a.spp; s0 += pl.pass_spp, ++k) {
+    const uint32_t h = overlap ? (k & 1u) : 0u;      // the scratch half (and overflow region) of the pass
+    const hipStream_t rs = h ? st->aux : stream;      // where it renders
+    const hipStream_t as = overlap ? st->acc : stream;  // where it is added
+    double* buf = reinterpret_cast<double*>(reinterpret_cast<char*>(scratch) + h * half_bytes);
+    uint32_t* queue = reinterpret_cast<uint32_t*>(buf + half_doubles);
     RenderArgs b = a;
     b.s_begin = s0;
     b.s_count = a.spp - s0 < pl.pass_spp ? a.spp - s0 : pl.pass_spp;
     b.chunk = pl.chunk;
     b.n_chunks = (b.s_count + pl.chunk - 1) / pl.chunk;
-    b.scratch = scratch;
+    b.scratch = buf;
     b.queue = queue;
     b.n_units = b.n_blocks * b.n_chunks;
     b.waves = (uint32_t)s->cu_count * 16;  // 4 waves per SIMD resident
+    if (a.stack_ovf) b.stack_ovf = a.stack_ovf + h * ovf_words;
     b.progress_base = base;
     base += b.n_units;
+    if (overlap && k >= 2) HIP_TRY(hipStreamWaitEvent(rs, st->ev_acc[h], 0), "hipStreamWaitEvent");
     // the unit counter, and the 8 XCD-local ones of mesh frames (kernels.hip, claim of a unit)
-    HIP_TRY(hipMemsetAsync(queue, 0, 9 * sizeof(uint32_t), stream), "zero the unit counters");
-    HIP_TRY(hipEventRecord(ev[3 * k], stream), "hipEventRecord");
-    HIP_TRY(launch_render(s->dev, b, stats, stream), "launch k_render");
-    HIP_TRY(hipEventRecord(ev[3 * k + 1], stream), "hipEventRecord");
-    HIP_TRY(launch_accumulate(b, s0 == 0, stream), "launch k_accumulate");
-    HIP_TRY(hipEventRecord(ev[3 * k + 2], stream), "hipEventRecord");
+    HIP_TRY(hipMemsetAsync(queue, 0, 9 * sizeof(uint32_t), rs), "zero the unit counters");
+    HIP_TRY(hipEventRecord(ev[3 * k], rs), "hipEventRecord");
+    HIP_TRY(launch_render(s->dev, b, stats, rs), "launch k_render");
+    HIP_TRY(hipEventRecord(ev[3 * k + 1], rs), "hipEventRecord");
+    if (overlap) {
+      HIP_TRY(hipEventRecord(st->ev_render[h], rs), "hipEventRecord");
+      HIP_TRY(hipStreamWaitEvent(as, st->ev_render[h], 0), "hipStreamWaitEvent");
+    }
+    HIP_TRY(launch_accumulate(b, s0 == 0, as), "launch k_accumulate");
+    HIP_TRY(hipEventRecord(ev[3 * k + 2], as), "hipEventRecord");
+    if (overlap) HIP_TRY(hipEventRecord(st->ev_acc[h], as), "hipEventRecord");
   }
+  if (overlap) HIP_TRY(hipStreamWaitEvent(stream, st->ev_acc[(passes - 1) & 1u], 0), "hipStreamWaitEvent");
   if (prog) prog->total_units = base;
   push_frame(s, stream, std::move(ev));
   return YART_OK;

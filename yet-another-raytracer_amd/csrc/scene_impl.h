@@ -50,6 +50,11 @@ struct StreamState {
   // deep meshes on the megakernel: the walk stacks' HBM overflow, kOvfWords per wave of a launch
   uint32_t* ovf = nullptr;
   size_t ovf_bytes = 0;
+  // frames of more than one scratch pass (capi.cpp launch_frame): the odd passes render on `aux`
+  // into the scratch's second half while the even ones finish on the caller's stream, and `acc`
+  // adds the passes in order; created with the stream's first such frame
+  hipStream_t aux = nullptr, acc = nullptr;
+  hipEvent_t ev_start = nullptr, ev_render[2] = {nullptr, nullptr}, ev_acc[2] = {nullptr, nullptr};
 };
 
 // Progress of one frame (yart_render's callback): the kernels store `base + units handed out` to
