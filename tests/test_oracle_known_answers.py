@@ -229,6 +229,40 @@ def test_sin_cos_within_one_ulp_of_libm():
     assert worst <= 1
 
 
+def _ulps(a, b):
+    return abs(struct.unpack("<q", struct.pack("<d", a))[0] - struct.unpack("<q", struct.pack("<d", b))[0])
+
+
+def test_libm_twins_against_this_hosts_glibc_on_the_draw_domains():
+    """What the fdlibm twins (oracle.c = kernels.hip, bitwise) differ by from the libm the reference
+    links on Linux (glibc; Rust's f64::sin / cos / ln / acos / atan2 call it), on the inputs the path
+    feeds them: sin / cos of 2 pi r (cosine and sphere-light sampling), ln of a uniform draw
+    (ConstantMedium's free path), acos / atan2 of unit-vector components (sphere uv). At most 1 ulp
+    everywhere; the share of values that differ, measured with this container's glibc 2.35 (which is
+    itself not correctly rounded on 0.24 % of the sin / cos inputs), is what DESIGN.md §2 states:
+    sin / cos ~3 %, ln ~7 %, acos ~8 %, atan2 ~18 %. The reference's own generator is unseedable, so
+    these last-ulp differences sit far inside the statistical comparison (test_statistical.py)."""
+    rng = np.random.default_rng(11)
+    L = O.lib()
+    n = 40000
+    r = rng.integers(0, 1 << 53, n, dtype=np.int64).astype(np.float64) * 2.0 ** -53
+    shares = {}
+    for name, cases in (
+            ("sin", [(L.oracle_sin(2.0 * math.pi * x), math.sin(2.0 * math.pi * x)) for x in r]),
+            ("cos", [(L.oracle_cos(2.0 * math.pi * x), math.cos(2.0 * math.pi * x)) for x in r]),
+            ("ln", [(L.oracle_log(1.0 - x), math.log(1.0 - x)) for x in r]),
+            ("acos", [(L.oracle_acos(2.0 * x - 1.0), math.acos(2.0 * x - 1.0)) for x in r])):
+        ulps = [_ulps(a, b) for a, b in cases]
+        assert max(ulps) <= 1, name
+        shares[name] = sum(u != 0 for u in ulps) / n
+    yx = rng.uniform(-1.0, 1.0, (n, 2))
+    ulps = [_ulps(L.oracle_atan2(y, x), math.atan2(y, x)) for y, x in yx]
+    assert max(ulps) <= 1
+    shares["atan2"] = sum(u != 0 for u in ulps) / n
+    assert 0.01 < shares["sin"] < 0.06 and 0.01 < shares["cos"] < 0.06, shares
+    assert shares["ln"] < 0.12 and shares["acos"] < 0.12 and shares["atan2"] < 0.25, shares
+
+
 def test_coverage_skips_row_224_of_a_225_row_image():  # main.rs:643-646
     m = O.coverage(400, 225)
     assert m[:224].all() and not m[224].any()
