@@ -98,6 +98,8 @@ struct Ieee {
   __device__ __forceinline__ double sqrt(double x) { return ::sqrt(x); }
   __device__ __forceinline__ double len(V3 a) { return ::sqrt(len2(a)); }
   __device__ __forceinline__ V3 unit(V3 a) { return yart_dev::unit(a); }
+  // unit(a) and len(a) (the same sqrt) from one evaluation
+  __device__ __forceinline__ V3 unit_len(V3 a, double& l) { l = len(a); return mk(a.x / l, a.y / l, a.z / l); }
   __device__ __forceinline__ PosDen den(double d) { return PosDen{d, 0.0}; }
   __device__ __forceinline__ double quo(double n, const PosDen& p) { return n / p.d; }
 };
@@ -120,9 +122,15 @@ struct Fast {
     return div_core_pos(n, p.d, p.r);
   }
   __device__ __forceinline__ V3 unit(V3 a) {
+    double l;
+    return unit_len(a, l);
+  }
+  // l = len(a) as well: a checked l in [2^-300, 2^300] has l^2 inside the sqrt core's range, so the
+  // len() check passes wherever this one does
+  __device__ __forceinline__ V3 unit_len(V3 a, double& l) {
     // |a| in [2^-300, 2^300] (the den check) also covers the sqrt core's range: l2 tiny, zero,
     // infinite or NaN leave l outside it. The components are at most |a|: only the lower bound.
-    const double l = sqrt_core(len2(a));
+    l = sqrt_core(len2(a));
     bad |= !(l >= 0x1p-300 && l <= 0x1p300);
     bad |= !(a.x == 0.0 || fabs(a.x) >= 0x1p-600);
     bad |= !(a.y == 0.0 || fabs(a.y) >= 0x1p-600);
@@ -1916,22 +1924,24 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& g, M& m) {  // pdf.rs
   const double sr2 = m.sqrt(r2);
   return mk(c * sr2, s * sr2, z);
 }
-template <class M>
-__device__ __forceinline__ double cosine_value(const Onb& b, V3 d, M& m) {  // pdf.rs:40-47
-  const double cosine = dot(m.unit(d), b.w);
+// ud = unit_vector(direction), formed once per scatter by the caller (it also feeds Lambertian's
+// scatter_pdf and a rect light's pdf its length): the same values, one evaluation
+__device__ __forceinline__ double cosine_value(const Onb& b, V3 ud) {  // pdf.rs:40-47
+  const double cosine = dot(ud, b.w);
   return cosine <= 0.0 ? 0.0 : cosine / kPi;
 }
 
 // pdf_value of a light that was hit (or not) at t over [0.001, inf) by (origin, dir).
 template <class M>
-__device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3 dir, bool hit, double t, M& m) {
+// ldir = dir.length(), formed by the caller with unit_vector(dir) (scatter_at)
+__device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3 dir, double ldir, bool hit, double t, M& m) {
   if (!hit) return 0.0;
   if (o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:148-162
     Hit h;
     rect_rec(1, Ray{origin, dir, 0.0, 0.0}, t, h);
     const double area = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
     const double distance_squared = h.t * h.t * len2(dir);
-    const double cosine = fabs(dot(dir, h.n)) / m.len(dir);
+    const double cosine = fabs(dot(dir, h.n)) / ldir;
     return distance_squared / (cosine * area);
   }
   // sphere.rs:95-110
@@ -1941,7 +1951,7 @@ __device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3
   return 1.0 / solid_angle;
 }
 template <bool STATS, class M>
-__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double wl, Stats& st, M& m) {
+__device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double ldir, double wl, Stats& st, M& m) {
   if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
   Ray r{origin, dir, 0.0, wl};
   double t = 0.0;
@@ -1955,7 +1965,7 @@ __device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 di
   } else {
     return 0.0;
   }
-  return light_pdf_at(o, origin, dir, hit, t, m);
+  return light_pdf_at(o, origin, dir, ldir, hit, t, m);
 }
 template <class M>
 __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g, M& m) {
@@ -2201,12 +2211,14 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
     // spilled) through the direction sampling and the light pdfs
     auto att = [&]() { return texture_value<EXT>(S, m.texture, wbin, hp, hu, hv); };
     const Onb uvw = onb_from_w(hn, mp);
-    V3 dir;
+    V3 dir, udir;  // the scattered direction and unit_vector(dir)
+    double ldir;   // dir.length()
     double pdf_val;
     if (S.n_lights == 0) {
       (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
       dir = local(uvw, random_cosine_direction(g, mp));
-      pdf_val = 0.5 * cosine_value(uvw, dir, mp) + 0.5 * cosine_value(uvw, dir, mp);
+      udir = mp.unit_len(dir, ldir);
+      pdf_val = 0.5 * cosine_value(uvw, udir) + 0.5 * cosine_value(uvw, udir);
     } else {
       if (gen_range(g, 0.0, 1.0) < 0.5) {
         // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
@@ -2221,14 +2233,16 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       }
       const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
       double sum = -0.0;
-      for (uint32_t i = 0; i < S.n_lights; ++i) sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ray.wl, st, mp);
-      pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, dir, mp);
+      udir = mp.unit_len(dir, ldir);
+      for (uint32_t i = 0; i < S.n_lights; ++i)
+        sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ldir, ray.wl, st, mp);
+      pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, udir);
     }
     if (!isfinite(pdf_val) || pdf_val <= 0.0) {
       R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
       term_ = true;
     } else {
-      const double cosine = dot(hn, mp.unit(dir));  // Lambertian::scatter_pdf
+      const double cosine = dot(hn, udir);  // Lambertian::scatter_pdf
       const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
       T_ = ((T * att()) * spdf) / pdf_val;
       o_ = hp;
