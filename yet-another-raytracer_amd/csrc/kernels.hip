@@ -1926,14 +1926,16 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& g, M& m) {  // pdf.rs
 }
 // ud = unit_vector(direction), formed once per scatter by the caller (it also feeds Lambertian's
 // scatter_pdf and a rect light's pdf its length): the same values, one evaluation
+// ud = unit_vector(direction). (Dividing by pi with the Fast core's hoisted reciprocal chain instead
+// of the IEEE divide cost the cornell box 1.5 %: registers; profiles/r06x_ab_picore.log.)
 __device__ __forceinline__ double cosine_value(const Onb& b, V3 ud) {  // pdf.rs:40-47
   const double cosine = dot(ud, b.w);
   return cosine <= 0.0 ? 0.0 : cosine / kPi;
 }
 
 // pdf_value of a light that was hit (or not) at t over [0.001, inf) by (origin, dir).
-template <class M>
-// ldir = dir.length(), formed by the caller with unit_vector(dir) (scatter_at)
+// ldir = dir.length(), formed by the caller with unit_vector(dir) (scatter_at); LEN: formed here
+template <bool LEN, class M>
 __device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3 dir, double ldir, bool hit, double t, M& m) {
   if (!hit) return 0.0;
   if (o.kind == YART_PRIM_XZ_RECT) {  // aarect.rs:148-162
@@ -1941,7 +1943,7 @@ __device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3
     rect_rec(1, Ray{origin, dir, 0.0, 0.0}, t, h);
     const double area = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
     const double distance_squared = h.t * h.t * len2(dir);
-    const double cosine = fabs(dot(dir, h.n)) / ldir;
+    const double cosine = fabs(dot(dir, h.n)) / (LEN ? m.len(dir) : ldir);
     return distance_squared / (cosine * area);
   }
   // sphere.rs:95-110
@@ -1950,7 +1952,7 @@ __device__ __forceinline__ double light_pdf_at(const DevObject& o, V3 origin, V3
   const double solid_angle = 2.0 * kPi * (1.0 - cos_theta_max);
   return 1.0 / solid_angle;
 }
-template <bool STATS, class M>
+template <bool STATS, bool LEN, class M>
 __device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 dir, double ldir, double wl, Stats& st, M& m) {
   if (o.n_xf != 0) return 0.0;  // wrappers do not override Hittable::pdf_value (hittable.rs:28-30)
   Ray r{origin, dir, 0.0, wl};
@@ -1965,7 +1967,7 @@ __device__ __forceinline__ double light_pdf(const DevObject& o, V3 origin, V3 di
   } else {
     return 0.0;
   }
-  return light_pdf_at(o, origin, dir, ldir, hit, t, m);
+  return light_pdf_at<LEN>(o, origin, dir, ldir, hit, t, m);
 }
 template <class M>
 __device__ __forceinline__ V3 light_random(const DevObject& o, V3 origin, Rng& g, M& m) {
@@ -2195,7 +2197,7 @@ constexpr int kMeshWavesPerEu = 4;
 // next ray and throughput, or its end. One body for both math policies (the Fast cores first; a
 // lane whose operand left a core's range re-runs it on the IEEE sequences from the same inputs
 // and the same draws) and for both render paths (k_render's fused loop, k_wf_shade).
-template <bool EXT, bool STATS, class MP>
+template <bool EXT, bool STATS, bool SHARE, class MP>
 __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, const V3& hp, const V3& hn, uint32_t hmat,
                                            double hu, double hv, int wbin, const Ray& ray, double T, uint32_t depth,
                                            Stats& st, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_,
@@ -2231,18 +2233,26 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       } else {
         dir = local(uvw, random_cosine_direction(g, mp));
       }
-      const double weight = 1.0 / (double)S.n_lights;  // hittable.rs:103-111
+      // hittable.rs:103-111 (formed on the host and read from the scene record instead, it cost david
+      // 0.8 %: profiles/r06x_ab_devweight.log)
+      const double weight = 1.0 / (double)S.n_lights;
       double sum = -0.0;
-      udir = mp.unit_len(dir, ldir);
+      // SHARE: unit_vector(dir) and its length once for the cosine pdf, the scatter pdf and a rect
+      // light's pdf, which evaluated them separately (the compiler did not merge them): cornell
+      // +2.1 %, random-scene +1.6 %; the mesh kernels keep the separate forms (david -0.7 %:
+      // registers; profiles/r06w_ab_unit_reuse.log, r06x_ab_picore.log)
+      if (SHARE) udir = mp.unit_len(dir, ldir);
+      else ldir = 0.0;
       for (uint32_t i = 0; i < S.n_lights; ++i)
-        sum = sum + weight * light_pdf<STATS>(uniform_at(S.lights, i), hp, dir, ldir, ray.wl, st, mp);
+        sum = sum + weight * light_pdf<STATS, !SHARE>(uniform_at(S.lights, i), hp, dir, ldir, ray.wl, st, mp);
+      if (!SHARE) udir = mp.unit(dir);
       pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, udir);
     }
     if (!isfinite(pdf_val) || pdf_val <= 0.0) {
       R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
       term_ = true;
     } else {
-      const double cosine = dot(hn, udir);  // Lambertian::scatter_pdf
+      const double cosine = dot(hn, SHARE ? udir : mp.unit(dir));  // Lambertian::scatter_pdf
       const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
       T_ = ((T * att()) * spdf) / pdf_val;
       o_ = hp;
@@ -2513,7 +2523,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
         // One body, two math policies: the Fast cores first; a lane with an operand outside a
         // core's range re-runs it on the IEEE sequences from the same inputs and the same draws.
         auto scatter = [&](auto& mp, double& T_, V3& o_, V3& d_, uint32_t& depth_, double& R_, bool& term_) {
-          scatter_at<EXT, STATS>(S, mp, g, hp, hn, hmat, hu, hv, wbin, ray, T, depth, st, T_, o_, d_, depth_, R_, term_);
+          scatter_at<EXT, STATS, !HAS_MESH>(S, mp, g, hp, hn, hmat, hu, hv, wbin, ray, T, depth, st, T_, o_, d_, depth_, R_, term_);
         };
         double nT, nR;
         V3 no, nd;
@@ -2708,7 +2718,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
         uint32_t ndepth;
         bool nterm;
         Ieee im;
-        scatter_at<false, false>(S, im, g, h.p, h.n, h.mat, 0.0, 0.0, wbin, ray, T, depth, st, nT, no, nd, ndepth, nR, nterm);
+        scatter_at<false, false, false>(S, im, g, h.p, h.n, h.mat, 0.0, 0.0, wbin, ray, T, depth, st, nT, no, nd, ndepth, nR, nterm);
         if (nterm) {
           R = nR;
           term = true;
