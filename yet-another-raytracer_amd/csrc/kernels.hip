@@ -602,44 +602,13 @@ __device__ __forceinline__ bool rect_hit(const double* p, const Ray& r, double t
 }
 __device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<1, 0, 2>(p, r, a, b, h); }
 
-// Conservative f32 slab pre-test for BoxEntity (not in the reference; exact by construction): a
-// face hit's computed point lies within a few f64 ulps of the box, so a ray whose parameter
-// range misses the box grown by m = 2^-12 (|box| + |origin|) cannot hit any face, and the six f64
-// face tests may be skipped. f32 rounding (~1e-7 relative) stays far inside m; rays with
-// non-finite components, or a direction component too small for f32, are never culled.
-__device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
-  const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
-  const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
-  const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
-  if (!(fabsf(chk) <= 3.0e38f)) return true;  // NaN / inf / near-overflow: do not cull
-  // A ray lying exactly in a face's plane (d[a] == 0, o[a] == the face's k) gets t = 0 / 0 = NaN in
-  // rect_t, and a NaN t passes its range and bounds tests: the reference "hits" that face wherever
-  // the ray runs. Such rays (an exactly zero direction component) are never culled.
-  if (r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0) return true;
-  const float bmn[3] = {fminf((float)p[0], (float)p[3]), fminf((float)p[1], (float)p[4]), fminf((float)p[2], (float)p[5])};
-  const float bmx[3] = {fmaxf((float)p[0], (float)p[3]), fmaxf((float)p[1], (float)p[4]), fmaxf((float)p[2], (float)p[5])};
-  const float B = fmaxf(fmaxf(fmaxf(fabsf(bmn[0]), fabsf(bmn[1])), fmaxf(fabsf(bmn[2]), fabsf(bmx[0]))),
-                        fmaxf(fabsf(bmx[1]), fabsf(bmx[2])));
-  const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
-  const float m = (B + O) * 0x1p-12f;
-  float lo = (float)tmin, hi = (float)tmax;
-  if (fabsf(lo) < INFINITY) lo = lo - fabsf(lo) * 0x1p-10f;  // an infinite bound stays as it is
-  if (fabsf(hi) < INFINITY) hi = hi + fabsf(hi) * 0x1p-10f;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    // slab unconstrained: a NaN reciprocal, which fmaxf / fminf (maxNum / minNum) ignore
-    const float inv = fabsf(d[j]) >= 1.0e-20f ? __builtin_amdgcn_rcpf(d[j]) : __builtin_nanf("");
-    const float t0 = (bmn[j] - m - o[j]) * inv, t1 = (bmx[j] + m - o[j]) * inv;
-    lo = fmaxf(lo, fminf(t0, t1));
-    hi = fminf(hi, fmaxf(t0, t1));
-  }
-  return lo <= hi;
-}
-
 // BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
 // 4-5 yz, so the face's plane axis is 2 - face / 2.
+// (r06: the conservative f32 slab pre-test that used to skip the six face tests of a ray missing the
+// box cost more than it saved — a wave runs the face tests whenever one lane needs them: cornell
+// 800x800x256 +2.0 %, cornell-box-smoke +6.9 % without it, bitwise; profiles/r06z_ab_nocull256.log.
+// In the world-BVH kernel the node boxes already cull per lane.)
 __device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face) {
-  if (!box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
   double closest = tmax, tt;
   double s[5];
@@ -1730,7 +1699,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
   const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
   // Non-finite rays, and rays with an exactly zero direction component (which can lie in a rect's
-  // plane, where rect_t's NaN t "hits" it outside any box, see box_may_hit), take the list walk.
+  // plane, where rect_t's NaN t "hits" it outside any box: aarect.rs:111-146), take the list walk.
   bool in_plane = r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0;
   // The same in the frames of the rotated rects and boxes: there a direction component can cancel to
   // exactly 0 while no world component is 0 (cos 90° d_x == d_z). Rays near those directions
