@@ -602,13 +602,50 @@ __device__ __forceinline__ bool rect_hit(const double* p, const Ray& r, double t
 }
 __device__ __forceinline__ bool xz_hit(const double* p, const Ray& r, double a, double b, Hit& h) { return rect_hit<1, 0, 2>(p, r, a, b, h); }
 
+// Conservative f32 slab pre-test for BoxEntity (not in the reference; exact by construction): a
+// face hit's computed point lies within a few f64 ulps of the box, so a ray whose parameter
+// range misses the box grown by m = 2^-12 (|box| + |origin|) cannot hit any face, and the six f64
+// face tests may be skipped. f32 rounding (~1e-7 relative) stays far inside m; rays with
+// non-finite components, or a direction component too small for f32, are never culled.
+__device__ __forceinline__ bool box_may_hit(const double* p, const Ray& r, double tmin, double tmax) {
+  const float o[3] = {(float)r.o.x, (float)r.o.y, (float)r.o.z};
+  const float d[3] = {(float)r.d.x, (float)r.d.y, (float)r.d.z};
+  const float chk = o[0] + o[1] + o[2] + d[0] + d[1] + d[2];
+  if (!(fabsf(chk) <= 3.0e38f)) return true;  // NaN / inf / near-overflow: do not cull
+  // A ray lying exactly in a face's plane (d[a] == 0, o[a] == the face's k) gets t = 0 / 0 = NaN in
+  // rect_t, and a NaN t passes its range and bounds tests: the reference "hits" that face wherever
+  // the ray runs. Such rays (an exactly zero direction component) are never culled.
+  if (r.d.x == 0.0 || r.d.y == 0.0 || r.d.z == 0.0) return true;
+  const float bmn[3] = {fminf((float)p[0], (float)p[3]), fminf((float)p[1], (float)p[4]), fminf((float)p[2], (float)p[5])};
+  const float bmx[3] = {fmaxf((float)p[0], (float)p[3]), fmaxf((float)p[1], (float)p[4]), fmaxf((float)p[2], (float)p[5])};
+  const float B = fmaxf(fmaxf(fmaxf(fabsf(bmn[0]), fabsf(bmn[1])), fmaxf(fabsf(bmn[2]), fabsf(bmx[0]))),
+                        fmaxf(fabsf(bmx[1]), fabsf(bmx[2])));
+  const float O = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
+  const float m = (B + O) * 0x1p-12f;
+  float lo = (float)tmin, hi = (float)tmax;
+  if (fabsf(lo) < INFINITY) lo = lo - fabsf(lo) * 0x1p-10f;  // an infinite bound stays as it is
+  if (fabsf(hi) < INFINITY) hi = hi + fabsf(hi) * 0x1p-10f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    // slab unconstrained: a NaN reciprocal, which fmaxf / fminf (maxNum / minNum) ignore
+    const float inv = fabsf(d[j]) >= 1.0e-20f ? __builtin_amdgcn_rcpf(d[j]) : __builtin_nanf("");
+    const float t0 = (bmn[j] - m - o[j]) * inv, t1 = (bmx[j] + m - o[j]) * inv;
+    lo = fmaxf(lo, fminf(t0, t1));
+    hi = fminf(hi, fmaxf(t0, t1));
+  }
+  return lo <= hi;
+}
+
 // BoxEntity (box_entity.rs:53-70): its six rects in order, closest first; `face` 0-1 xy, 2-3 xz,
 // 4-5 yz, so the face's plane axis is 2 - face / 2.
-// (r06: the conservative f32 slab pre-test that used to skip the six face tests of a ray missing the
-// box cost more than it saved — a wave runs the face tests whenever one lane needs them: cornell
-// 800x800x256 +2.0 %, cornell-box-smoke +6.9 % without it, bitwise; profiles/r06z_ab_nocull256.log.
-// In the world-BVH kernel the node boxes already cull per lane.)
+// CULL: the f32 pre-test first. The list kernels go without it (r06): their wave runs the six face
+// tests whenever one lane needs them, so the test was pure cost there — cornell 800x800x256 +2.0 %,
+// cornell-box-smoke +6.9 % without it, bitwise. The mesh and world-BVH kernels keep it: without it
+// their code came out slower (david -2.4 %, bunny -0.8 %, random-scene -0.6 %; same box,
+// profiles/r06z_ab_nocull256.log, r06z_ab_mesh_nocull.log).
+template <bool CULL = true>
 __device__ __forceinline__ bool box_t(const double* p, const Ray& r, double tmin, double tmax, double& t, uint32_t& face) {
+  if (CULL && !box_may_hit(p, r, tmin, tmax)) return false;
   bool found = false;
   double closest = tmax, tt;
   double s[5];
@@ -1483,7 +1520,9 @@ __device__ __forceinline__ void mesh_rec(const DevMesh& M, const Ray& r, double 
 // u, v; the mesh kernels carry u, v and the triangle (a mesh hit's walk result) through the pass.
 struct HitId { double t, u, v; uint32_t obj, sub; };
 
-template <bool HAS_MESH, bool STATS, bool OVF = false>
+// CULL: the box entity's f32 pre-test (box_t); off in the list kernels (HAS_MESH false), on in the
+// mesh and world-BVH kernels
+template <bool HAS_MESH, bool STATS, bool OVF = false, bool CULL = HAS_MESH>
 __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, uint32_t kind, const Ray& r,
                                        double tmin, double tmax, double& t, uint32_t& sub, double& u, double& v,
                                        uint32_t* stk, Stats& st, uint32_t* ovf = nullptr) {
@@ -1492,7 +1531,7 @@ __device__ __forceinline__ bool prim_t(const DevScene& S, const DevObject& o, ui
     case YART_PRIM_XY_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<2, 0, 1>(o.p, r, tmin, tmax, t);
     case YART_PRIM_XZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<1, 0, 2>(o.p, r, tmin, tmax, t);
     case YART_PRIM_YZ_RECT: if (STATS) st.v[ST_PRIM]++; return rect_t<0, 1, 2>(o.p, r, tmin, tmax, t);
-    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t(o.p, r, tmin, tmax, t, sub);
+    case YART_PRIM_BOX: if (STATS) st.v[ST_PRIM] += 6; return box_t<CULL>(o.p, r, tmin, tmax, t, sub);
     case YART_PRIM_TRIANGLE: if (STATS) st.v[ST_PRIM]++; return triangle_t(o.p, r, tmin, tmax, t, u, v);
     case YART_PRIM_MOVING_SPHERE: if (STATS) st.v[ST_PRIM]++; return moving_sphere_t(o.p, r, tmin, tmax, t);
     case YART_PRIM_MESH:
@@ -1565,7 +1604,8 @@ __device__ __forceinline__ const T& uniform_at(const T* base, uint32_t i) {
   return *(const T*)((cptr)base + __builtin_amdgcn_readfirstlane(i));
 }
 
-template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false, bool PARK = false>
+template <bool HAS_MESH, bool STATS, bool EXT, int SLOTS = kCoopSlots, bool OVF = false, bool PARK = false,
+          bool CULL = HAS_MESH>
 __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, const Ray& r, double tmin, double tmax, HitId& id,
                                               uint32_t* stk, uint8_t* coop, Stats& st, const QueryCtx& q,
                                               uint32_t* ovf = nullptr, bool resume = false, bool* parked = nullptr) {
@@ -1595,7 +1635,7 @@ __device__ __forceinline__ bool world_closest(const DevScene& S, bool want, cons
       double t, u = 0.0, v = 0.0;
       uint32_t sub = 0;
       const bool hit = medium ? medium_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, r, tmin, closest, t, stk, st, q, i, ovf)
-                              : prim_t<HAS_MESH, STATS, OVF>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, ovf);
+                              : prim_t<HAS_MESH, STATS, OVF, CULL>(S, o, kind, lr, tmin, closest, t, sub, u, v, stk, st, ovf);
       if (hit) {
         closest = t;
         if (HAS_MESH) { id.obj = i; id.sub = sub; id.u = u; id.v = v; }
@@ -1706,7 +1746,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   // (DevScene::plane_dirs) take the list walk too. 0 entries in scenes without rotated planes.
   if (S.n_plane_dirs) in_plane = in_plane || near_plane_dir(S, r.d.x, r.d.z);
   if (!(fabsf(chk) <= 3.0e38f) || in_plane)
-    return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
+    return world_closest<false, STATS, false, kCoopSlots, false, false, true>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
   float inv[3];
   bool use[3];
 #pragma unroll
@@ -1724,7 +1764,8 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
   // overflow (|o| |1/d| near the f32 range) takes the list walk.
   const float mr = O * 0x1p-12f;
   const float imax = fmaxf(fmaxf(fabsf(inv[0]), fabsf(inv[1])), fabsf(inv[2]));
-  if (!((O + mr) * imax <= 1.0e37f)) return world_closest<false, STATS, false>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
+  if (!((O + mr) * imax <= 1.0e37f))
+    return world_closest<false, STATS, false, kCoopSlots, false, false, true>(S, true, r, tmin, tmax, id, stk, nullptr, st, QueryCtx{});
   float ca[3], cb[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) { ca[j] = -((o[j] + mr) * inv[j]); cb[j] = (mr - o[j]) * inv[j]; }
@@ -1778,7 +1819,7 @@ __device__ __forceinline__ bool world_closest_bvh(const DevScene& S, const Ray& 
           const Ray lr = to_local(ob, ob.n_xf, r);
           double t, u = 0.0, v = 0.0;
           uint32_t sub = 0;
-          if (prim_t<false, STATS>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
+          if (prim_t<false, STATS, false, true>(S, ob, ob.kind, lr, tmin, closest, t, sub, u, v, stk, st) &&
               (!found || t < closest || (i << 3) > who)) {
             closest = t;
             who = (i << 3) | sub;
