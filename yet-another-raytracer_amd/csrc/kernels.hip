@@ -464,8 +464,28 @@ __device__ __forceinline__ uint64_t gen_index(Rng& r, uint64_t n) {  // UniformI
 }
 
 // ----------------------------------------------------------------------------- spectra
+// x / d for a constant d through the division core with r = RN(1/d) written out (Markstein: one
+// fma correction of RN(x r) is the correctly rounded quotient whenever r is within half an ulp of
+// 1/d and x is neither tiny nor huge): the IEEE quotient in 3 VALU instructions instead of 11.
+// The constants are made opaque at each use, so they are not hoisted into registers held through
+// the render loop. YART_CONST_DIV=0 builds the plain divides.
+#ifndef YART_CONST_DIV
+#define YART_CONST_DIV 1
+#endif
+constexpr double kRcpBinWidth = 0x1.999999999999ap-4;  // RN(1 / 10)
+constexpr double kRcpPi = 0x1.45f306dc9c883p-2;        // RN(1 / kPi)
+__device__ __forceinline__ double div_const(double x, double d, double r) {
+  asm volatile("" : "+s"(d), "+s"(r));
+  return div_core_pos(x, d, r);
+}
+// CDIV: the constant-divisor core — in the list and world-BVH kernels without EXT features (cornell
+// +0.6 %, random-scene +0.7 % same box, profiles/r06f4_ab_constdiv.log); in the mesh kernels it
+// raised the spills (74 -> 112 scratch sites), in the EXT list kernel cornell-box-smoke -0.7 %
+template <bool CDIV>
 __device__ __forceinline__ int spectrum_bin(double wl) {  // color.rs:276-283
-  double f = (wl - kMinLambda) / kBinWidth;
+  // wl - 360 is 0 or at least ulp(360) ~ 6e-14 here (wl from gen_range over [360, 720)), inside
+  // the core's range
+  double f = (CDIV && YART_CONST_DIV) ? div_const(wl - kMinLambda, kBinWidth, kRcpBinWidth) : (wl - kMinLambda) / kBinWidth;
   if (!(f > 0.0)) return 0;
   if (f >= 36.0) return 35;
   return (int)f;
@@ -1936,11 +1956,21 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& g, M& m) {  // pdf.rs
 }
 // ud = unit_vector(direction), formed once per scatter by the caller (it also feeds Lambertian's
 // scatter_pdf and a rect light's pdf its length): the same values, one evaluation
-// ud = unit_vector(direction). (Dividing by pi with the Fast core's hoisted reciprocal chain instead
-// of the IEEE divide cost the cornell box 1.5 %: registers; profiles/r06x_ab_picore.log.)
-__device__ __forceinline__ double cosine_value(const Onb& b, V3 ud) {  // pdf.rs:40-47
+// x / pi through the policy with pi's reciprocal as a constant (div_const; the Fast policy checks x's
+// range and re-runs the block on the IEEE sequences outside it). (The reciprocal formed by rcp_core
+// and hoisted out of the loop instead cost the cornell box 1.5 %: registers; r06x_ab_picore.log.)
+template <bool CDIV, class M>
+__device__ __forceinline__ double over_pi(double x, M& m) {
+  if (!CDIV || !YART_CONST_DIV) return x / kPi;
+  double d = kPi, r = kRcpPi;
+  asm volatile("" : "+s"(d), "+s"(r));
+  return m.quo(x, PosDen{d, r});
+}
+// ud = unit_vector(direction)
+template <bool CDIV, class M>
+__device__ __forceinline__ double cosine_value(const Onb& b, V3 ud, M& m) {  // pdf.rs:40-47
   const double cosine = dot(ud, b.w);
-  return cosine <= 0.0 ? 0.0 : cosine / kPi;
+  return cosine <= 0.0 ? 0.0 : over_pi<CDIV>(cosine, m);
 }
 
 // pdf_value of a light that was hit (or not) at t over [0.001, inf) by (origin, dir).
@@ -2230,7 +2260,7 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       (void)gen_range(g, 0.0, 1.0);  // MixurePDF(cos, cos): both branches sample the cosine
       dir = local(uvw, random_cosine_direction(g, mp));
       udir = mp.unit_len(dir, ldir);
-      pdf_val = 0.5 * cosine_value(uvw, udir) + 0.5 * cosine_value(uvw, udir);
+      pdf_val = 0.5 * cosine_value<SHARE && !EXT>(uvw, udir, mp) + 0.5 * cosine_value<SHARE && !EXT>(uvw, udir, mp);
     } else {
       if (gen_range(g, 0.0, 1.0) < 0.5) {
         // HittableList::random (hittable.rs:113-122): 0..len-1 never picks the last light
@@ -2256,14 +2286,14 @@ __device__ __forceinline__ void scatter_at(const DevScene& S, MP& mp, Rng& g, co
       for (uint32_t i = 0; i < S.n_lights; ++i)
         sum = sum + weight * light_pdf<STATS, !SHARE>(uniform_at(S.lights, i), hp, dir, ldir, ray.wl, st, mp);
       if (!SHARE) udir = mp.unit(dir);
-      pdf_val = 0.5 * sum + 0.5 * cosine_value(uvw, udir);
+      pdf_val = 0.5 * sum + 0.5 * cosine_value<SHARE && !EXT>(uvw, udir, mp);
     }
     if (!isfinite(pdf_val) || pdf_val <= 0.0) {
       R_ = T * 0.0;  // Lambertian::emitted is 0 (material.rs:25-27)
       term_ = true;
     } else {
       const double cosine = dot(hn, SHARE ? udir : mp.unit(dir));  // Lambertian::scatter_pdf
-      const double spdf = cosine < 0.0 ? 0.0 : cosine / kPi;
+      const double spdf = cosine < 0.0 ? 0.0 : over_pi<SHARE && !EXT>(cosine, mp);
       T_ = ((T * att()) * spdf) / pdf_val;
       o_ = hp;
       d_ = dir;
@@ -2525,7 +2555,7 @@ __global__ __launch_bounds__(256, HAS_MESH ? kMeshWavesPerEu : kWavesPerEu) void
         const double v = 1.0 - ty / (double)hm1;
         const double wl = gen_range(g, kMinLambda, kMaxLambda);  // gen_wavelength color.rs:20-23
         ray = camera_ray(*kernarg_camera(), u, v, wl, g, EXT && S.has_time);
-        wbin = spectrum_bin(wl);  // the path's reflectance bin (color.rs:276-283), once per sample
+        wbin = spectrum_bin<!HAS_MESH && !EXT>(wl);  // the path's reflectance bin (color.rs:276-283), once per sample
         T = 1.0;
         depth = A.max_depth;
         fresh = false;
@@ -2705,7 +2735,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(DevScene S, RenderArgs A, WfAr
     depth = Q.depth[i]; T = Q.T[i]; ray.wl = Q.wl[i];
     ray.o = mk(Q.o[i], Q.o[P + i], Q.o[2 * (size_t)P + i]);
     ray.d = mk(Q.d[i], Q.d[P + i], Q.d[2 * (size_t)P + i]);
-    const int wbin = spectrum_bin(ray.wl);
+    const int wbin = spectrum_bin<false>(ray.wl);
     const uint32_t obj = Q.hobj[i];
     double R = 0.0;
     bool term = false;
