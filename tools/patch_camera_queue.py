@@ -57,7 +57,7 @@ rep('''          if ((cov >> slot) & 1ull) { fresh = true; need = false; }''',
               ray.d = mk(e[192], e[256], e[320]);
               ray.wl = e[384];
               ray.time = kernarg_camera()->time0;
-              wbin = spectrum_bin(ray.wl);
+              wbin = spectrum_bin<!HAS_MESH && !EXT>(ray.wl);
               T = 1.0;
               depth = A.max_depth;
             }
